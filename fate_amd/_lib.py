@@ -1,0 +1,95 @@
+"""ctypes binding of libfatephe.so (include/fate_phe.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (or ``make -C fate_amd``)
+into ``fate_amd/lib/libfatephe.so``.  There is no CPU fallback: if the shared object
+is missing or a HIP device is absent, every compute entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libfatephe.so")
+
+FPHE_OK = 0
+FPHE_ERR_ARG = 1
+FPHE_ERR_HIP = 2
+FPHE_ERR_NO_SK = 3
+FPHE_ERR_KEY = 4
+
+EF_ENCODE_NONFINITE = 0x01
+EF_DECODE_CORRUPTED = 0x02
+EF_DECODE_OVERFLOW = 0x04
+EF_MUL_INVALID_PT = 0x08
+EF_NOT_INVERTIBLE = 0x10
+
+# every symbol declared in include/fate_phe.h
+EXPORTED_SYMBOLS = (
+    "fphe_ctx_create", "fphe_ctx_destroy", "fphe_ctx_limbs",
+    "fphe_encode_f32", "fphe_encode_f64", "fphe_decode_f32", "fphe_decode_f64",
+    "fphe_encrypt", "fphe_decrypt", "fphe_add", "fphe_mul",
+)
+
+_lock = threading.Lock()
+_lib: Optional[ctypes.CDLL] = None
+
+c_u32p = ctypes.POINTER(ctypes.c_uint32)
+vp = ctypes.c_void_p
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+def load() -> ctypes.CDLL:
+    """Load (once) and type the native library.  Raises NativeLibraryMissing."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise NativeLibraryMissing(
+                f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+        lib = ctypes.CDLL(LIB_PATH)
+        st = ctypes.c_int
+        lib.fphe_ctx_create.argtypes = [ctypes.c_int, ctypes.c_uint32, c_u32p, c_u32p, c_u32p, ctypes.POINTER(vp)]
+        lib.fphe_ctx_create.restype = st
+        lib.fphe_ctx_destroy.argtypes = [vp]
+        lib.fphe_ctx_destroy.restype = st
+        lib.fphe_ctx_limbs.argtypes = [vp, c_u32p, c_u32p]
+        lib.fphe_ctx_limbs.restype = st
+        for name in ("fphe_encode_f32", "fphe_encode_f64"):
+            f = getattr(lib, name)
+            f.argtypes = [vp, vp, ctypes.c_size_t, vp, vp, vp, vp, vp]
+            f.restype = st
+        for name in ("fphe_decode_f32", "fphe_decode_f64"):
+            f = getattr(lib, name)
+            f.argtypes = [vp, vp, ctypes.c_uint32, vp, ctypes.c_size_t, vp, vp, vp]
+            f.restype = st
+        lib.fphe_encrypt.argtypes = [vp, vp, ctypes.c_uint32, vp, ctypes.c_size_t, ctypes.c_int, vp,
+                                     c_u32p, ctypes.c_uint64, vp, vp, vp]
+        lib.fphe_encrypt.restype = st
+        lib.fphe_decrypt.argtypes = [vp, vp, ctypes.c_size_t, vp, vp]
+        lib.fphe_decrypt.restype = st
+        lib.fphe_add.argtypes = [vp, vp, vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_size_t, vp, vp, vp, vp]
+        lib.fphe_add.restype = st
+        lib.fphe_mul.argtypes = [vp, vp, vp, vp, vp, ctypes.c_uint32, vp, vp, ctypes.c_int, ctypes.c_size_t,
+                                 vp, vp, vp, vp, vp]
+        lib.fphe_mul.restype = st
+        _lib = lib
+        return lib
+
+
+def check(status: int, what: str) -> None:
+    if status == FPHE_OK:
+        return
+    if status == FPHE_ERR_ARG:
+        raise ValueError(f"{what}: invalid argument")
+    if status == FPHE_ERR_NO_SK:
+        raise ValueError(f"{what}: context has no private key")
+    if status == FPHE_ERR_KEY:
+        raise ValueError(f"{what}: key material rejected")
+    raise RuntimeError(f"{what}: HIP runtime error (status {status})")

@@ -1,0 +1,1020 @@
+// libfatephe: MI355X-native Paillier PHE kernels + C ABI (include/fate_phe.h).
+//
+// Reference semantics: rust/fate_utils/crates/paillier/src/lib.rs (L0) and
+// rust/fate_utils/crates/fixedpoint_paillier/src/lib.rs (L1); SURVEY.md Appendix A.
+// Every kernel processes one element per lane (TPI = 1) with a grid-stride loop over
+// 64-element wave groups; see DESIGN.md for the layout and roofline of each kernel.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+#include <vector>
+#include <mutex>
+
+#include "../../include/fate_phe.h"
+#include "mont_dev.h"
+#include "chacha_dev.h"
+#include "host_bn.h"
+
+using namespace fphe;
+
+namespace {
+
+constexpr int kBlock = 256;      // 4 waves per workgroup
+constexpr int kWavesPerBlock = kBlock / FPHE_WAVE;
+constexpr int kWinEnc = 5;       // window of the shared-exponent modexps (r^n, c^(p-1))
+constexpr int kWinMul = 4;       // window of the per-lane-exponent modexp (ct x pt)
+
+// Uniform key material, passed by value (lands in the kernarg segment -> SGPRs).
+struct KeyArgs {
+  const u32* N2;       // n^2                     [L2]
+  const u32* N2_R2;    // R^2 mod n^2, R=2^(32 L2) [L2]
+  const u32* N2_R1;    // R mod n^2 (Montgomery 1) [L2]
+  const u32* n;        // n, padded               [L1+1]
+  const u32* nm1;      // n-1                     [L1]
+  const u32* max_int;  // floor(n/2)              [L1]
+  const u32* n_mm;     // n - max_int             [L1]
+  u32 n2_n0inv;
+  int nbits;
+  // private half (valid iff has_sk)
+  const u32* P2; const u32* P2_R3; const u32* pm1; const u32* p; const u32* pinv2; const u32* hpR;
+  const u32* Q2; const u32* Q2_R3; const u32* qm1; const u32* q; const u32* qinv2; const u32* hqR;
+  const u32* pinvqR;   // p^{-1} mod q, times R_q mod q
+  u32 p2_n0inv, p_n0inv, q2_n0inv, q_n0inv;
+  int pm1_bits, qm1_bits;
+};
+
+__device__ __forceinline__ void set_err(int32_t* err, u32 f) {
+  if (f) atomicOr(err, (int32_t)f);
+}
+
+// Per-kernel geometry: one 64-element tile per wave per grid-stride step.
+struct WaveCtx {
+  int lane;
+  u32 gw, nw;  // global wave id, waves in grid (both wave-uniform)
+};
+
+__device__ __forceinline__ WaveCtx wave_ctx() {
+  WaveCtx w;
+  w.lane = (int)(threadIdx.x & 63);
+  const u32 wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  w.gw = blockIdx.x * kWavesPerBlock + wib;
+  w.nw = gridDim.x * kWavesPerBlock;
+  return w;
+}
+
+template <int L>
+__device__ __forceinline__ u32* lds_slot(u32* lds, int lane) {
+  const u32 wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  return lds + wib * L * FPHE_WAVE + lane;
+}
+
+// ======================================================================================
+// encrypt: C = (1 + m*n mod n^2) * r^n mod n^2, sign = (m < 0)
+//   crates/paillier/src/lib.rs:104-121; both branches of :106-113 reduce to 1 + m*n
+//   mod n^2 (the invert branch computes inv(1 - (n-m)n) = 1 + m n), and the sign of
+//   the truncating product at :116 is the sign of m (r^n > 0).
+// ======================================================================================
+template <int L>
+__device__ __forceinline__ bool nude_to_slot(u32* slot, const KeyArgs& K, const Tile& Pt, u32 lp, bool negflag) {
+  constexpr int L1 = L / 2;
+#pragma unroll
+  for (int j = 0; j < L; ++j) slot[j * FPHE_WAVE] = 0u;
+  u32 any = 0;
+#pragma unroll 1
+  for (u32 k = 0; k < lp; ++k) {
+    const u32 pk = Pt.ld(k * 256u);
+    any |= pk;
+    u64 acc = 0;
+#pragma unroll
+    for (int j = 0; j < L1; ++j) {
+      u32* s = slot + (k + j) * FPHE_WAVE;
+      acc = (u64)pk * K.n[j] + *s + (acc >> 32);
+      *s = (u32)acc;
+    }
+    slot[(k + L1) * FPHE_WAVE] = (u32)(acc >> 32);
+  }
+  const bool mneg = negflag && (any != 0);
+  if (mneg) {  // n^2 - |m| n
+    u32 br = 0;
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      u32* s = slot + j * FPHE_WAVE;
+      const u64 d = (u64)K.N2[j] - *s - br;
+      *s = (u32)d;
+      br = (u32)(d >> 63);
+    }
+  }
+  u32 c = 1;  // + 1
+#pragma unroll
+  for (int j = 0; j < L; ++j) {
+    u32* s = slot + j * FPHE_WAVE;
+    const u64 t = (u64)*s + c;
+    *s = (u32)t;
+    c = (u32)(t >> 32);
+  }
+  return mneg;
+}
+
+template <int L>
+__device__ __forceinline__ void draw_r(u32 (&A)[L], const KeyArgs& K, const ChaChaKey& ck, u64 nonce, size_t e) {
+  constexpr int L1 = L / 2;
+  constexpr int NB = (L1 + 15) / 16;
+  const int topbits = K.nbits - 32 * (L1 - 1);
+  const u32 topmask = topbits >= 32 ? 0xffffffffu : ((1u << topbits) - 1u);
+#pragma unroll
+  for (int j = L1; j < L; ++j) A[j] = 0;
+  bool done = false;
+  u32 attempt = 0;
+  while (__any(!done)) {
+    if (!done) {
+      u32 x[L1];
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        u32 blk[16];
+        chacha20_block(ck, attempt * NB + b, (u32)e, (u32)(nonce >> 32), (u32)nonce, blk);
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (b * 16 + i < L1) x[b * 16 + i] = blk[i];
+      }
+      x[L1 - 1] &= topmask;
+      // accept iff x < n - 1, then r = x + 1 in [1, n-1]  (random.rs:22-25)
+      u32 br = 0;
+#pragma unroll
+      for (int j = 0; j < L1; ++j) {
+        const u64 d = (u64)x[j] - K.nm1[j] - br;
+        br = (u32)(d >> 63);
+      }
+      if (br) {
+        u32 c = 1;
+#pragma unroll
+        for (int j = 0; j < L1; ++j) {
+          const u64 t = (u64)x[j] + c;
+          A[j] = (u32)t;
+          c = (u32)(t >> 32);
+        }
+        done = true;
+      }
+    }
+    ++attempt;
+  }
+}
+
+template <int L, int W>
+__global__ __launch_bounds__(kBlock) void k_encrypt(KeyArgs K, const u32* __restrict__ P, u32 lp,
+                                                    const u8* __restrict__ neg, u32 ntiles, int obf,
+                                                    const u32* __restrict__ rin, ChaChaKey ck, u64 nonce,
+                                                    u32* __restrict__ Cout, u8* __restrict__ sout,
+                                                    u32* __restrict__ scratch) {
+  constexpr int L1 = L / 2;
+  extern __shared__ __attribute__((aligned(16))) u32 lds[];
+  const WaveCtx w = wave_ctx();
+  u32* slot = lds_slot<L>(lds, w.lane);
+  const Tile tb = make_tile(scratch + (size_t)w.gw * ((size_t)(1 << W) * L * FPHE_WAVE), (1u << W) * L * 256u, w.lane);
+  for (u32 tile = w.gw; tile < ntiles; tile += w.nw) {
+    const size_t e = (size_t)tile * FPHE_WAVE + w.lane;
+    const Tile Pt = make_tile(P + (size_t)tile * lp * FPHE_WAVE, lp * 256u, w.lane);
+    const Tile Ct = make_tile(Cout + (size_t)tile * L * FPHE_WAVE, L * 256u, w.lane);
+    const bool mneg = nude_to_slot<L>(slot, K, Pt, lp, neg[e] != 0);
+    if (!obf) {
+#pragma unroll
+      for (int j = 0; j < L; ++j) Ct.st(slot[j * FPHE_WAVE], j * 256u);
+      sout[e] = mneg ? 1 : 0;
+      continue;
+    }
+    // stash C_nude in table entry 0 (powm_uniform uses entries 1 .. 2^W-1)
+#pragma unroll
+    for (int j = 0; j < L; ++j) tb.st(slot[j * FPHE_WAVE], j * 256u);
+    u32 A[L];
+    if (rin) {
+      const Tile Rt = make_tile(rin + (size_t)tile * L1 * FPHE_WAVE, L1 * 256u, w.lane);
+#pragma unroll
+      for (int j = 0; j < L1; ++j) A[j] = Rt.ld(j * 256u);
+#pragma unroll
+      for (int j = L1; j < L; ++j) A[j] = 0;
+    } else {
+      draw_r<L>(A, K, ck, nonce, e);
+    }
+    slot_store_uniform<L>(slot, K.N2_R2);
+    mont_mul<L>(A, slot, K.N2, K.n2_n0inv);                           // r R
+    powm_uniform<L, W>(A, slot, tb, K.N2, K.n2_n0inv, K.n, K.nbits);  // r^n R
+    tile_to_slot<L>(slot, tb, 0u);
+    mont_mul<L>(A, slot, K.N2, K.n2_n0inv);                           // r^n * C_nude
+    tile_store<L>(Ct, 0u, A);
+    sout[e] = mneg ? 1 : 0;
+  }
+}
+
+// ======================================================================================
+// decrypt (CRT): crates/paillier/src/lib.rs:163-176
+// ======================================================================================
+// d_s = L_s(c^(s-1) mod s^2) * h_s mod s  for s in {p, q}
+template <int L, int W>
+__device__ __forceinline__ void crt_half(u32 (&dout)[L / 4], const Tile& Cin, u32* slot, const Tile& tb,
+                                         const u32* __restrict__ S2, u32 s2_n0inv, const u32* __restrict__ S2_R3,
+                                         const u32* __restrict__ sm1, int sm1_bits, const u32* __restrict__ S,
+                                         u32 s_n0inv, const u32* __restrict__ sinv2, const u32* __restrict__ hsR) {
+  constexpr int LH = L / 2, LQ = L / 4;
+  u32 A[LH];
+  {
+    // REDC of the 2LH-limb c modulo S2 (c < n^2 < S2 * 2^(32 LH))
+    u32 T[L + 1];
+#pragma unroll
+    for (int j = 0; j < L; ++j) T[j] = Cin.ld(j * 256u);
+    T[L] = 0;
+#pragma unroll 1
+    for (int i = 0; i < LH; ++i) {
+      const u32 m = T[0] * s2_n0inv;
+      u64 acc = (u64)m * S2[0] + T[0];
+#pragma unroll
+      for (int j = 1; j < LH; ++j) {
+        acc = (u64)m * S2[j] + T[j] + (acc >> 32);
+        T[j - 1] = (u32)acc;
+      }
+#pragma unroll
+      for (int j = LH; j <= L; ++j) {
+        acc = (u64)T[j] + (acc >> 32);
+        T[j - 1] = (u32)acc;
+      }
+      T[L] = (u32)(acc >> 32);
+    }
+    u32 br = 0;
+#pragma unroll
+    for (int j = 0; j < LH; ++j) {
+      const u64 d = (u64)T[j] - S2[j] - br;
+      A[j] = (u32)d;
+      br = (u32)(d >> 63);
+    }
+    const bool keep = (T[LH] == 0) & (br != 0);
+#pragma unroll
+    for (int j = 0; j < LH; ++j) A[j] = keep ? T[j] : A[j];
+  }
+  slot_store_uniform<LH>(slot, S2_R3);
+  mont_mul<LH>(A, slot, S2, s2_n0inv);                            // c R mod s^2
+  powm_uniform<LH, W>(A, slot, tb, S2, s2_n0inv, sm1, sm1_bits);  // c^(s-1) R
+  slot_store_small<LH>(slot, 1u);
+  mont_mul<LH>(A, slot, S2, s2_n0inv);                            // y = c^(s-1) mod s^2
+  // L(y) = (y - 1) / s, exact for units: (y-1) * s^{-1} mod 2^(32 LQ)
+  u32 nz = 0;
+#pragma unroll
+  for (int j = 0; j < LH; ++j) nz |= A[j];
+  u32 y1[LQ];
+  {
+    u32 br = 1;
+#pragma unroll
+    for (int j = 0; j < LQ; ++j) {
+      const u64 d = (u64)A[j] - br;
+      y1[j] = (u32)d;
+      br = (u32)(d >> 63);
+    }
+  }
+  u32 Ls[LQ];
+#pragma unroll
+  for (int j = 0; j < LQ; ++j) Ls[j] = 0;
+#pragma unroll
+  for (int i = 0; i < LQ; ++i) {
+    u64 acc = 0;
+#pragma unroll
+    for (int j = 0; i + j < LQ; ++j) {
+      acc = (u64)y1[i] * sinv2[j] + Ls[i + j] + (acc >> 32);
+      Ls[i + j] = (u32)acc;
+    }
+  }
+  if (nz == 0) {  // y == 0: reference computes (0-1)/s = 0 (truncating)
+#pragma unroll
+    for (int j = 0; j < LQ; ++j) Ls[j] = 0;
+  }
+  slot_store_uniform<LQ>(slot, hsR);
+  mont_mul<LQ>(Ls, slot, S, s_n0inv);  // L * h_s mod s
+#pragma unroll
+  for (int j = 0; j < LQ; ++j) dout[j] = Ls[j];
+}
+
+template <int L, int W>
+__global__ __launch_bounds__(kBlock) void k_decrypt(KeyArgs K, const u32* __restrict__ C, u32 ntiles,
+                                                    u32* __restrict__ Pout, u32* __restrict__ scratch) {
+  constexpr int LH = L / 2, LQ = L / 4;
+  extern __shared__ __attribute__((aligned(16))) u32 lds[];
+  const WaveCtx w = wave_ctx();
+  u32* slot = lds_slot<LH>(lds, w.lane);
+  const Tile tb = make_tile(scratch + (size_t)w.gw * ((size_t)(1 << W) * LH * FPHE_WAVE), (1u << W) * LH * 256u, w.lane);
+  for (u32 tile = w.gw; tile < ntiles; tile += w.nw) {
+    const Tile Cin = make_tile(C + (size_t)tile * L * FPHE_WAVE, L * 256u, w.lane);
+    const Tile Pt = make_tile(Pout + (size_t)tile * LH * FPHE_WAVE, LH * 256u, w.lane);
+    u32 dp[LQ], dq[LQ];
+    crt_half<L, W>(dp, Cin, slot, tb, K.P2, K.p2_n0inv, K.P2_R3, K.pm1, K.pm1_bits, K.p, K.p_n0inv, K.pinv2, K.hpR);
+    crt_half<L, W>(dq, Cin, slot, tb, K.Q2, K.q2_n0inv, K.Q2_R3, K.qm1, K.qm1_bits, K.q, K.q_n0inv, K.qinv2, K.hqR);
+    // u = (dq - dp) mod q ; u = u * p^{-1} mod q  (paillier/src/lib.rs:166, canonical form; the
+    // reference's `if o < 0 { o += n }` at :168-170 lands on the same value)
+    u32 u[LQ];
+    u32 br = 0;
+#pragma unroll
+    for (int j = 0; j < LQ; ++j) {
+      const u64 d = (u64)dq[j] - dp[j] - br;
+      u[j] = (u32)d;
+      br = (u32)(d >> 63);
+    }
+    if (br) {
+      u32 c = 0;
+#pragma unroll
+      for (int j = 0; j < LQ; ++j) {
+        const u64 t = (u64)u[j] + K.q[j] + c;
+        u[j] = (u32)t;
+        c = (u32)(t >> 32);
+      }
+    }
+    slot_store_uniform<LQ>(slot, K.pinvqR);
+    mont_mul<LQ>(u, slot, K.q, K.q_n0inv);
+    // m = u * p + dp  (p uniform outer operand, shifting accumulator; limb i final after step i)
+    u32 T[LQ + 1];
+#pragma unroll
+    for (int j = 0; j < LQ; ++j) T[j] = dp[j];
+    T[LQ] = 0;
+#pragma unroll 1
+    for (int i = 0; i < LQ; ++i) {
+      const u32 pi = K.p[i];
+      u64 acc = 0;
+#pragma unroll
+      for (int j = 0; j < LQ; ++j) {
+        acc = (u64)u[j] * pi + T[j] + (acc >> 32);
+        T[j] = (u32)acc;
+      }
+      T[LQ] += (u32)(acc >> 32);
+      Pt.st(T[0], (u32)i * 256u);
+#pragma unroll
+      for (int j = 0; j < LQ; ++j) T[j] = T[j + 1];
+      T[LQ] = 0;
+    }
+#pragma unroll
+    for (int j = 0; j < LQ; ++j) Pt.st(T[j], (u32)(LQ + j) * 256u);
+  }
+}
+
+// ======================================================================================
+// add: Ciphertext::add (fixedpoint_paillier/src/lib.rs:301-333) with decrese_exp_to
+// (:250-258): the higher-exp operand x is raised to 16^d = 2^(4d) (4d Montgomery
+// squarings), then multiplied into y; sign = XOR of the operands at the final product.
+// ======================================================================================
+template <int L>
+__global__ __launch_bounds__(kBlock) void k_add(KeyArgs K, const u32* __restrict__ Ca, const u8* __restrict__ sa,
+                                                const int32_t* __restrict__ ea, const u32* __restrict__ Cb,
+                                                const u8* __restrict__ sb, const int32_t* __restrict__ eb,
+                                                int bstride, u32 ntiles, u32* __restrict__ Co,
+                                                u8* __restrict__ so, int32_t* __restrict__ eo) {
+  extern __shared__ __attribute__((aligned(16))) u32 lds[];
+  const WaveCtx w = wave_ctx();
+  u32* slot = lds_slot<L>(lds, w.lane);
+  for (u32 tile = w.gw; tile < ntiles; tile += w.nw) {
+    const size_t e = (size_t)tile * FPHE_WAVE + w.lane;
+    const size_t be = bstride ? e : 0;
+    const Tile At = make_tile(Ca + (size_t)tile * L * FPHE_WAVE, L * 256u, w.lane);
+    const Tile Bt = bstride ? make_tile(Cb + (size_t)tile * L * FPHE_WAVE, L * 256u, w.lane)
+                            : make_tile(Cb, L * 256u, 0);
+    const Tile Ot = make_tile(Co + (size_t)tile * L * FPHE_WAVE, L * 256u, w.lane);
+    const int xa = ea[e], xb = eb[be];
+    const u32 sav = sa[e], sbv = sb[be];
+    const bool x_is_a = xa > xb;
+    u32 A[L];
+    u32 ra = 0, rb = 0;
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      const u32 va = At.ld(j * 256u), vb = Bt.ld(j * 256u);
+      ra |= j == 0 ? (va ^ 1u) : va;
+      rb |= j == 0 ? (vb ^ 1u) : vb;
+      A[j] = x_is_a ? va : vb;
+    }
+    // literal-1 tests (:303-308): the signed integer equals 1 iff sign == 0 and C == 1
+    const bool lit_a = (ra == 0) && (sav == 0);
+    const bool lit_b = (rb == 0) && (sbv == 0);
+    int d = x_is_a ? xa - xb : xb - xa;
+    if (lit_a || lit_b) d = 0;
+    slot_store_uniform<L>(slot, K.N2_R2);
+    mont_mul<L>(A, slot, K.N2, K.n2_n0inv);  // x R
+    const int nsq = wave_max_int(4 * d);
+#pragma unroll 1
+    for (int k = 0; k < nsq; ++k) {
+      if (k < 4 * d) mont_sqr<L>(A, slot, K.N2, K.n2_n0inv);
+    }
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      const u32 va = At.ld(j * 256u), vb = Bt.ld(j * 256u);
+      slot[j * FPHE_WAVE] = x_is_a ? vb : va;
+    }
+    mont_mul<L>(A, slot, K.N2, K.n2_n0inv);  // x^(16^d) * y mod n^2
+    const u32 sy = x_is_a ? sbv : sav;
+    u32 sign = d == 0 ? (sav ^ sbv) : sy;
+    int exo = xa < xb ? xa : xb;
+    if (lit_a || lit_b) {
+#pragma unroll
+      for (int j = 0; j < L; ++j) {
+        const u32 va = At.ld(j * 256u), vb = Bt.ld(j * 256u);
+        A[j] = lit_a ? vb : va;
+      }
+      sign = lit_a ? sbv : sav;
+      exo = lit_a ? xb : xa;
+    }
+    tile_store<L>(Ot, 0u, A);
+    so[e] = (u8)sign;
+    eo[e] = exo;
+  }
+}
+
+// ======================================================================================
+// mul: Ciphertext::mul (fixedpoint_paillier/src/lib.rs:334-349): c^b mod n^2 with a
+// per-lane exponent b (fixed window over the wave's longest exponent), exp = e_c + e_b.
+// ======================================================================================
+template <int L, int W>
+__global__ __launch_bounds__(kBlock) void k_mul(KeyArgs K, const u32* __restrict__ Ca, const u8* __restrict__ sa,
+                                                const int32_t* __restrict__ ea, const u32* __restrict__ P, u32 lp,
+                                                const u8* __restrict__ pneg, const int32_t* __restrict__ pexp,
+                                                int pstride, size_t count, u32* __restrict__ Co,
+                                                u8* __restrict__ so, int32_t* __restrict__ eo,
+                                                int32_t* __restrict__ err, u32* __restrict__ scratch) {
+  const u32 ntiles = (u32)((count + FPHE_WAVE - 1) / FPHE_WAVE);
+  constexpr int L1 = L / 2;
+  constexpr u32 TE = L * 256u;
+  extern __shared__ __attribute__((aligned(16))) u32 lds[];
+  const WaveCtx w = wave_ctx();
+  u32* slot = lds_slot<L>(lds, w.lane);
+  const Tile tb = make_tile(scratch + (size_t)w.gw * ((size_t)(1 << W) * L * FPHE_WAVE), (1u << W) * TE, w.lane);
+  for (u32 tile = w.gw; tile < ntiles; tile += w.nw) {
+    const size_t e = (size_t)tile * FPHE_WAVE + w.lane;
+    const size_t pe = pstride ? e : 0;
+    const Tile Pt = pstride ? make_tile(P + (size_t)tile * lp * FPHE_WAVE, lp * 256u, w.lane)
+                            : make_tile(P, lp * 256u, 0);
+    const Tile At = make_tile(Ca + (size_t)tile * L * FPHE_WAVE, L * 256u, w.lane);
+    const Tile Ot = make_tile(Co + (size_t)tile * L * FPHE_WAVE, L * 256u, w.lane);
+    // classify the plaintext significand (:335-344)
+    u32 any = 0;
+    int ebits = 0;
+    u32 br_max = 0, br_nmm = 0;  // borrows of max_int - P and P - n_mm
+#pragma unroll 4
+    for (int j = 0; j < L1; ++j) {
+      const u32 pj = (u32)j < lp ? Pt.ld((u32)j * 256u) : 0u;
+      any |= pj;
+      if (pj) ebits = 32 * j + 32 - __clz(pj);
+      const u64 d1 = (u64)K.max_int[j] - pj - br_max;
+      br_max = (u32)(d1 >> 63);
+      const u64 d2 = (u64)pj - K.n_mm[j] - br_nmm;
+      br_nmm = (u32)(d2 >> 63);
+    }
+    const bool isneg = (pneg[pe] != 0) && (any != 0);
+    const bool big = !isneg && (br_nmm == 0);              // P >= n - max_int
+    const bool invalid = !isneg && !big && (br_max != 0);  // P > max_int
+    u32 ef = 0;
+    if (isneg || big) ef |= FPHE_EF_NOT_INVERTIBLE;  // inverse branches: not yet on device
+    if (invalid) ef |= FPHE_EF_MUL_INVALID_PT;
+    if (e < count) set_err(err, ef);
+    if (isneg || big || invalid) ebits = 0;
+    const int maxbits = wave_max_int(ebits);
+    u32 A[L];
+    tile_load<L>(A, At, 0u);
+    slot_store_uniform<L>(slot, K.N2_R2);
+    mont_mul<L>(A, slot, K.N2, K.n2_n0inv);  // X = c R
+    if (maxbits > 0) {
+      slot_store<L>(slot, A);
+      tile_store<L>(tb, 1 * TE, A);
+#pragma unroll
+      for (int j = 0; j < L; ++j) tb.st(K.N2_R1[j], j * 256u);  // entry 0 = Montgomery 1
+#pragma unroll 1
+      for (int k = 2; k < (1 << W); ++k) {
+        mont_mul<L>(A, slot, K.N2, K.n2_n0inv);
+        tile_store<L>(tb, (u32)k * TE, A);
+      }
+      const int nwin = (maxbits + W - 1) / W;
+      auto digit = [&](int wi) -> u32 {
+        const int b0 = wi * W;
+        const u32 limb = (u32)(b0 >> 5);
+        const u32 v = limb < lp ? Pt.ld(limb * 256u) : 0u;
+        const u32 dd = (v >> (b0 & 31)) & ((1u << W) - 1);
+        return ebits == 0 ? 0u : dd;
+      };
+      // per-lane table entry: entry index differs by lane, so address it through the
+      // lane-varying voffset of the same (uniform) descriptor
+      auto entry_to = [&](u32 (&dst)[L], u32 dgt) {
+        Tile t = tb;
+        t.vo = tb.vo + dgt * TE;
+        tile_load<L>(dst, t, 0u);
+      };
+      entry_to(A, digit(nwin - 1));
+#pragma unroll 1
+      for (int wi = nwin - 2; wi >= 0; --wi) {
+#pragma unroll 1
+        for (int s = 0; s < W; ++s) mont_sqr<L>(A, slot, K.N2, K.n2_n0inv);
+        Tile t = tb;
+        t.vo = tb.vo + digit(wi) * TE;
+        tile_to_slot<L>(slot, t, 0u);
+        mont_mul<L>(A, slot, K.N2, K.n2_n0inv);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < L; ++j) A[j] = K.N2_R1[j];
+    }
+    slot_store_small<L>(slot, 1u);
+    mont_mul<L>(A, slot, K.N2, K.n2_n0inv);  // leave Montgomery form
+    tile_store<L>(Ot, 0u, A);
+    so[e] = 0;
+    eo[e] = ea[e] + pexp[pe];
+  }
+}
+
+// ======================================================================================
+// fixed-point encode / decode (fixedpoint_paillier/src/lib.rs:148-192)
+// ======================================================================================
+__device__ __forceinline__ size_t tiled(size_t e, u32 lp, u32 j) {
+  return ((e >> 6) * lp + j) * FPHE_WAVE + (e & 63);
+}
+
+__device__ __forceinline__ u32 encode_core(double x, u64& mag, bool& ng, int& ex) {
+  const u64 b = (u64)__double_as_longlong(x);
+  const int E = (int)((b >> 52) & 0x7ff);
+  const u64 frac = b & ((1ull << 52) - 1);
+  ng = (b >> 63) != 0;
+  if (E == 0x7ff) { mag = 0; ex = 0; ng = false; return FPHE_EF_ENCODE_NONFINITE; }
+  if (E == 0 && frac == 0) { mag = 0; ex = -14; ng = false; return 0; }  // frexp(0).1 = 0 -> exp=-14
+  int e;       // frexp exponent: x = f * 2^e, f in [0.5, 1)
+  int lsb;     // x = m * 2^lsb
+  u64 m;
+  if (E != 0) { m = frac | (1ull << 52); e = E - 1022; lsb = E - 1075; }
+  else { const int bl = 64 - __clzll(frac); m = frac; e = bl - 1074; lsb = -1074; }
+  ex = (e - 53) >> 2;         // floor((e-53)/4), arithmetic shift
+  mag = m << (lsb - 4 * ex);  // exact: x * 16^-ex  (round() is exact here)
+  return 0;
+}
+
+__global__ __launch_bounds__(256) void k_encode_f32(const float* __restrict__ x, size_t count, u32* __restrict__ P,
+                                                    u8* __restrict__ neg, int32_t* __restrict__ exp,
+                                                    int32_t* __restrict__ err) {
+  u32 ef = 0;
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < count; e += (size_t)gridDim.x * blockDim.x) {
+    u64 mag; bool ng; int ex;
+    ef |= encode_core((double)x[e], mag, ng, ex);
+    P[tiled(e, 2, 0)] = (u32)mag; P[tiled(e, 2, 1)] = (u32)(mag >> 32);
+    neg[e] = ng ? 1 : 0; exp[e] = ex;
+  }
+  set_err(err, ef);
+}
+
+__global__ __launch_bounds__(256) void k_encode_f64(const double* __restrict__ x, size_t count, u32* __restrict__ P,
+                                                    u8* __restrict__ neg, int32_t* __restrict__ exp,
+                                                    int32_t* __restrict__ err) {
+  u32 ef = 0;
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < count; e += (size_t)gridDim.x * blockDim.x) {
+    u64 mag; bool ng; int ex;
+    ef |= encode_core(x[e], mag, ng, ex);
+    P[tiled(e, 2, 0)] = (u32)mag; P[tiled(e, 2, 1)] = (u32)(mag >> 32);
+    neg[e] = ng ? 1 : 0; exp[e] = ex;
+  }
+  set_err(err, ef);
+}
+
+// decode_f64 (:169-186).  exp >= 0: (M << 4exp).to_f64() truncates (mpz_get_d);
+// exp < 0: M * Float(53)^exp is rounded to 53 bits (RNE) by MPFR, then to_f64 (RNE, a
+// second rounding only in the subnormal range).
+template <int L1>
+__device__ __forceinline__ double decode_core(const u32* __restrict__ P, u32 lp, size_t e, int ex,
+                                              const KeyArgs& K, u32& ef) {
+  u32 M[L1];
+  u32 br_n = 0, br_max = 0, br_nmm = 0;
+#pragma unroll
+  for (int j = 0; j < L1; ++j) {
+    M[j] = (u32)j < lp ? P[tiled(e, lp, j)] : 0u;
+    const u64 d0 = (u64)K.n[j] - M[j] - br_n; br_n = (u32)(d0 >> 63);        // n - P
+    const u64 d1 = (u64)K.max_int[j] - M[j] - br_max; br_max = (u32)(d1 >> 63);
+    const u64 d2 = (u64)M[j] - K.n_mm[j] - br_nmm; br_nmm = (u32)(d2 >> 63);
+  }
+  // limbs beyond L1 must be zero (P < 2^(32 L1)) else corrupted
+  u32 hi = 0;
+  for (u32 j = L1; j < lp; ++j) hi |= P[tiled(e, lp, j)];
+  if (br_n || hi) { ef |= FPHE_EF_DECODE_CORRUPTED; return 0.0; }
+  bool ng = false;
+  if (br_max == 0) {
+    // M <= max_int: mantissa = M
+  } else if (br_nmm == 0) {
+    ng = true;  // mantissa = M - n (negative): magnitude n - M
+    u32 br = 0;
+#pragma unroll
+    for (int j = 0; j < L1; ++j) {
+      const u64 d = (u64)K.n[j] - M[j] - br;
+      M[j] = (u32)d; br = (u32)(d >> 63);
+    }
+  } else {
+    ef |= FPHE_EF_DECODE_OVERFLOW; return 0.0;
+  }
+  // locate the top limb
+  int h = -1;
+#pragma unroll
+  for (int j = 0; j < L1; ++j) if (M[j]) h = j;
+  if (h < 0) return 0.0;
+  u32 w0 = 0, w1 = 0, w2 = 0, sticky = 0;
+#pragma unroll
+  for (int j = 0; j < L1; ++j) {
+    if (j == h) w0 = M[j];
+    if (j == h - 1) w1 = M[j];
+    if (j == h - 2) w2 = M[j];
+    if (j < h - 2) sticky |= M[j];
+  }
+  const int lz = __clz(w0);
+  const u64 top = ((u64)w0 << 32) | w1;
+  const u64 t64 = lz ? ((top << lz) | ((u64)w2 >> (32 - lz))) : top;
+  const u32 rest = lz ? (w2 << lz) : w2;
+  sticky |= rest;
+  int E2 = 32 * h + 31 - lz + 4 * ex;  // exponent of the leading bit
+  u64 mant = t64 >> 11;
+  if (ex < 0) {
+    const u32 low = (u32)(t64 & 0x7ff);
+    if (low > 0x400u || (low == 0x400u && (sticky || (mant & 1)))) ++mant;
+    if (mant >> 53) { mant >>= 1; ++E2; }
+  }
+  u64 bits;
+  if (E2 > 1023) {
+    bits = 0x7ff0000000000000ull;
+  } else if (E2 >= -1022) {
+    bits = ((u64)(E2 + 1023) << 52) | (mant & ((1ull << 52) - 1));
+  } else {
+    const int sh = -1022 - E2;
+    u64 q = 0;
+    if (sh <= 53) {
+      q = mant >> sh;
+      const u64 rem = mant & ((1ull << sh) - 1);
+      const u64 half = 1ull << (sh - 1);
+      if (rem > half || (rem == half && (q & 1))) ++q;
+    }
+    bits = q;
+  }
+  if (ng) bits |= 0x8000000000000000ull;
+  return __longlong_as_double((long long)bits);
+}
+
+template <int L1>
+__global__ __launch_bounds__(256) void k_decode_f32(KeyArgs K, const u32* __restrict__ P, u32 lp,
+                                                    const int32_t* __restrict__ exp, size_t count,
+                                                    float* __restrict__ out, int32_t* __restrict__ err) {
+  u32 ef = 0;
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < count; e += (size_t)gridDim.x * blockDim.x)
+    out[e] = __double2float_rn(decode_core<L1>(P, lp, e, exp[e], K, ef));
+  set_err(err, ef);
+}
+
+template <int L1>
+__global__ __launch_bounds__(256) void k_decode_f64(KeyArgs K, const u32* __restrict__ P, u32 lp,
+                                                    const int32_t* __restrict__ exp, size_t count,
+                                                    double* __restrict__ out, int32_t* __restrict__ err) {
+  u32 ef = 0;
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < count; e += (size_t)gridDim.x * blockDim.x)
+    out[e] = decode_core<L1>(P, lp, e, exp[e], K, ef);
+  set_err(err, ef);
+}
+
+}  // namespace
+
+// ======================================================================================
+// host side: context + C ABI
+// ======================================================================================
+struct fphe_ctx {
+  int device = 0;
+  uint32_t key_bits = 0;
+  int L2 = 0, L1 = 0, LQ = 0;
+  bool has_sk = false;
+  int cus = 0;
+  u32* blob = nullptr;
+  KeyArgs K{};
+  u32* scratch = nullptr;
+  size_t scratch_bytes = 0;
+  std::mutex mu;
+};
+
+namespace {
+
+using hbn::Limbs;
+
+fphe_status hip_ok(hipError_t e) { return e == hipSuccess ? FPHE_OK : FPHE_ERR_HIP; }
+
+struct DevGuard {
+  int prev = 0;
+  explicit DevGuard(int d) { (void)hipGetDevice(&prev); (void)hipSetDevice(d); }
+  ~DevGuard() { (void)hipSetDevice(prev); }
+};
+
+Limbs from_words(const uint32_t* w, size_t n) { return hbn::norm(Limbs(w, w + n)); }
+
+// Grid: `bpc` workgroups per CU (from LDS/VGPR budget), capped by the work.
+u32 ntiles_of(size_t count) { return (u32)((count + FPHE_WAVE - 1) / FPHE_WAVE); }
+
+unsigned grid_for(const fphe_ctx* c, size_t count, int bpc) {
+  const size_t groups = (count + kBlock - 1) / kBlock;  // 4 tiles per workgroup
+  size_t g = (size_t)c->cus * bpc;
+  if (groups < g) g = groups;
+  return (unsigned)(g ? g : 1);
+}
+
+fphe_status ensure_scratch(fphe_ctx* c, size_t bytes) {
+  if (c->scratch_bytes >= bytes) return FPHE_OK;
+  if (c->scratch) { (void)hipFree(c->scratch); c->scratch = nullptr; c->scratch_bytes = 0; }
+  if (hipMalloc(&c->scratch, bytes) != hipSuccess) return FPHE_ERR_HIP;
+  c->scratch_bytes = bytes;
+  return FPHE_OK;
+}
+
+template <typename KernT>
+void set_lds(KernT k, size_t bytes) {
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+// workgroups per CU for a kernel whose per-wave LDS slot is `slot_limbs` limbs
+int bpc_for_slot(int slot_limbs) {
+  const size_t per_block = (size_t)kWavesPerBlock * slot_limbs * FPHE_WAVE * 4;
+  int b = (int)((160 * 1024) / per_block);
+  return b < 1 ? 1 : (b > 2 ? 2 : b);
+}
+
+}  // namespace
+
+namespace {
+template <int L>
+fphe_status launch_encrypt(fphe_ctx* c, const uint32_t* P, uint32_t lp, const uint8_t* neg, size_t count,
+                                  int obf, const uint32_t* r, const uint32_t key[8], uint64_t nonce, uint32_t* C,
+                                  uint8_t* sign, hipStream_t s) {
+  const int bpc = bpc_for_slot(L);
+  const unsigned grid = grid_for(c, count, bpc);
+  const size_t lds = (size_t)kWavesPerBlock * L * FPHE_WAVE * 4;
+  const size_t sbytes = (size_t)grid * kWavesPerBlock * (1u << kWinEnc) * L * FPHE_WAVE * 4;
+  if (ensure_scratch(c, sbytes) != FPHE_OK) return FPHE_ERR_HIP;
+  ChaChaKey ck;
+  for (int i = 0; i < 8; ++i) ck.k[i] = key ? key[i] : 0u;
+  auto kern = k_encrypt<L, kWinEnc>;
+  set_lds(kern, lds);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, P, lp, neg, ntiles_of(count), obf, r, ck, nonce, C,
+                     sign, c->scratch);
+  return hip_ok(hipGetLastError());
+}
+
+template <int L>
+fphe_status launch_decrypt(fphe_ctx* c, const uint32_t* C, size_t count, uint32_t* P, hipStream_t s) {
+  constexpr int LH = L / 2;
+  const int bpc = bpc_for_slot(LH);
+  const unsigned grid = grid_for(c, count, bpc);
+  const size_t lds = (size_t)kWavesPerBlock * LH * FPHE_WAVE * 4;
+  const size_t sbytes = (size_t)grid * kWavesPerBlock * (1u << kWinEnc) * LH * FPHE_WAVE * 4;
+  if (ensure_scratch(c, sbytes) != FPHE_OK) return FPHE_ERR_HIP;
+  auto kern = k_decrypt<L, kWinEnc>;
+  set_lds(kern, lds);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, C, ntiles_of(count), P, c->scratch);
+  return hip_ok(hipGetLastError());
+}
+
+template <int L>
+fphe_status launch_add(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, const int32_t* ea,
+                              const uint32_t* Cb, const uint8_t* sb, const int32_t* eb, int bstride, size_t count,
+                              uint32_t* Co, uint8_t* so, int32_t* eo, hipStream_t s) {
+  const int bpc = bpc_for_slot(L);
+  const unsigned grid = grid_for(c, count, bpc);
+  const size_t lds = (size_t)kWavesPerBlock * L * FPHE_WAVE * 4;
+  auto kern = k_add<L>;
+  set_lds(kern, lds);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, Ca, sa, ea, Cb, sb, eb, bstride, ntiles_of(count), Co,
+                     so, eo);
+  return hip_ok(hipGetLastError());
+}
+
+template <int L>
+fphe_status launch_mul(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, const int32_t* ea,
+                              const uint32_t* P, uint32_t lp, const uint8_t* pneg, const int32_t* pexp, int pstride,
+                              size_t count, uint32_t* Co, uint8_t* so, int32_t* eo, int32_t* err, hipStream_t s) {
+  const int bpc = bpc_for_slot(L);
+  const unsigned grid = grid_for(c, count, bpc);
+  const size_t lds = (size_t)kWavesPerBlock * L * FPHE_WAVE * 4;
+  const size_t sbytes = (size_t)grid * kWavesPerBlock * (1u << kWinMul) * L * FPHE_WAVE * 4;
+  if (ensure_scratch(c, sbytes) != FPHE_OK) return FPHE_ERR_HIP;
+  auto kern = k_mul<L, kWinMul>;
+  set_lds(kern, lds);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, Ca, sa, ea, P, lp, pneg, pexp, pstride, count, Co,
+                     so, eo, err, c->scratch);
+  return hip_ok(hipGetLastError());
+}
+
+}  // namespace
+
+extern "C" {
+
+fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, const uint32_t* p_w,
+                            const uint32_t* q_w, fphe_ctx** out) {
+  if (!out || !n_w) return FPHE_ERR_ARG;
+  if (key_bits != 1024 && key_bits != 2048) return FPHE_ERR_ARG;
+  if ((p_w == nullptr) != (q_w == nullptr)) return FPHE_ERR_ARG;
+  const int L1 = key_bits / 32, L2 = 2 * L1, LQ = L1 / 2;
+  try {
+    Limbs n = from_words(n_w, L1);
+    if (n.empty() || !(n[0] & 1)) return FPHE_ERR_KEY;
+    if (hbn::bitlen(n) != key_bits) return FPHE_ERR_KEY;  // paillier/src/lib.rs:82 keeps bits(n)==k
+    Limbs N2 = hbn::mul(n, n);
+    std::vector<std::pair<const char*, Limbs>> arrays;
+    std::vector<u32> blob;
+    auto put = [&](const Limbs& v, size_t len) -> size_t {
+      const size_t off = blob.size();
+      Limbs p = hbn::padded(v, len);
+      blob.insert(blob.end(), p.begin(), p.end());
+      while (blob.size() % 4) blob.push_back(0);  // 16-byte aligned sections
+      return off;
+    };
+    const size_t o_N2 = put(N2, L2);
+    const size_t o_N2R2 = put(hbn::pow2_mod((size_t)64 * L2, N2), L2);
+    const size_t o_N2R1 = put(hbn::pow2_mod((size_t)32 * L2, N2), L2);
+    const size_t o_n = put(n, L1 + 1);
+    const size_t o_nm1 = put(hbn::sub(n, Limbs{1}), L1);
+    Limbs max_int = n;  // floor(n/2)
+    for (size_t i = 0; i < max_int.size(); ++i)
+      max_int[i] = (max_int[i] >> 1) | (i + 1 < max_int.size() ? max_int[i + 1] << 31 : 0);
+    max_int = hbn::norm(max_int);
+    const size_t o_max = put(max_int, L1);
+    const size_t o_nmm = put(hbn::sub(n, max_int), L1);
+    size_t o_P2 = 0, o_P2R3 = 0, o_pm1 = 0, o_p = 0, o_pinv2 = 0, o_hpR = 0;
+    size_t o_Q2 = 0, o_Q2R3 = 0, o_qm1 = 0, o_q = 0, o_qinv2 = 0, o_hqR = 0, o_pinvqR = 0;
+    u32 p2n0 = 0, pn0 = 0, q2n0 = 0, qn0 = 0;
+    int pm1b = 0, qm1b = 0;
+    const bool has_sk = p_w != nullptr;
+    if (has_sk) {
+      Limbs p = from_words(p_w, LQ), q = from_words(q_w, LQ);
+      if (hbn::cmp(p, q) == 0) return FPHE_ERR_KEY;
+      if (hbn::cmp(p, q) > 0) std::swap(p, q);  // SK::new keeps p < q (paillier/src/lib.rs:127)
+      if (hbn::cmp(hbn::mul(p, q), n) != 0) return FPHE_ERR_KEY;
+      if (!(p[0] & 1) || !(q[0] & 1)) return FPHE_ERR_KEY;
+      Limbs P2 = hbn::mul(p, p), Q2 = hbn::mul(q, q);
+      Limbs pm1 = hbn::sub(p, Limbs{1}), qm1 = hbn::sub(q, Limbs{1});
+      // h_p = ((g^(p-1) mod p^2 - 1)/p)^{-1} mod p with g = n+1 (paillier/src/lib.rs:131-137);
+      // (1+n)^(p-1) = 1 + (p-1) n (mod p^2), so the L-value is (p-1) q mod p.
+      auto hval = [&](const Limbs& s, const Limbs& t) {
+        Limbs Lv = hbn::mod(hbn::mul(hbn::sub(s, Limbs{1}), t), s);
+        return hbn::inv_mod(Lv, s);
+      };
+      Limbs hp = hval(p, q), hq = hval(q, p);
+      Limbs pinvq = hbn::inv_mod(p, q);
+      o_P2 = put(P2, L1);
+      o_P2R3 = put(hbn::pow2_mod((size_t)96 * L1, P2), L1);
+      o_pm1 = put(pm1, LQ + 1);
+      o_p = put(p, LQ);
+      o_pinv2 = put(hbn::inv_pow2(p, LQ), LQ);
+      o_hpR = put(hbn::mod(hbn::mul(hp, hbn::pow2_mod((size_t)32 * LQ, p)), p), LQ);
+      o_Q2 = put(Q2, L1);
+      o_Q2R3 = put(hbn::pow2_mod((size_t)96 * L1, Q2), L1);
+      o_qm1 = put(qm1, LQ + 1);
+      o_q = put(q, LQ);
+      o_qinv2 = put(hbn::inv_pow2(q, LQ), LQ);
+      o_hqR = put(hbn::mod(hbn::mul(hq, hbn::pow2_mod((size_t)32 * LQ, q)), q), LQ);
+      o_pinvqR = put(hbn::mod(hbn::mul(pinvq, hbn::pow2_mod((size_t)32 * LQ, q)), q), LQ);
+      p2n0 = hbn::neg_inv32(P2[0]); pn0 = hbn::neg_inv32(p[0]);
+      q2n0 = hbn::neg_inv32(Q2[0]); qn0 = hbn::neg_inv32(q[0]);
+      pm1b = (int)hbn::bitlen(pm1); qm1b = (int)hbn::bitlen(qm1);
+    }
+    auto* c = new fphe_ctx();
+    c->device = device; c->key_bits = key_bits; c->L1 = L1; c->L2 = L2; c->LQ = LQ; c->has_sk = has_sk;
+    DevGuard g(device);
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) { delete c; return FPHE_ERR_HIP; }
+    c->cus = prop.multiProcessorCount;
+    if (hipMalloc(&c->blob, blob.size() * 4) != hipSuccess) { delete c; return FPHE_ERR_HIP; }
+    if (hipMemcpy(c->blob, blob.data(), blob.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+      (void)hipFree(c->blob); delete c; return FPHE_ERR_HIP;
+    }
+    u32* b = c->blob;
+    KeyArgs& K = c->K;
+    K.N2 = b + o_N2; K.N2_R2 = b + o_N2R2; K.N2_R1 = b + o_N2R1; K.n = b + o_n; K.nm1 = b + o_nm1;
+    K.max_int = b + o_max; K.n_mm = b + o_nmm;
+    K.n2_n0inv = hbn::neg_inv32(N2[0]);
+    K.nbits = (int)key_bits;
+    if (has_sk) {
+      K.P2 = b + o_P2; K.P2_R3 = b + o_P2R3; K.pm1 = b + o_pm1; K.p = b + o_p; K.pinv2 = b + o_pinv2; K.hpR = b + o_hpR;
+      K.Q2 = b + o_Q2; K.Q2_R3 = b + o_Q2R3; K.qm1 = b + o_qm1; K.q = b + o_q; K.qinv2 = b + o_qinv2; K.hqR = b + o_hqR;
+      K.pinvqR = b + o_pinvqR;
+      K.p2_n0inv = p2n0; K.p_n0inv = pn0; K.q2_n0inv = q2n0; K.q_n0inv = qn0;
+      K.pm1_bits = pm1b; K.qm1_bits = qm1b;
+    }
+    *out = c;
+    return FPHE_OK;
+  } catch (...) {
+    return FPHE_ERR_KEY;
+  }
+}
+
+fphe_status fphe_ctx_destroy(fphe_ctx* c) {
+  if (!c) return FPHE_ERR_ARG;
+  {
+    DevGuard g(c->device);
+    if (c->blob) (void)hipFree(c->blob);
+    if (c->scratch) (void)hipFree(c->scratch);
+  }
+  delete c;
+  return FPHE_OK;
+}
+
+fphe_status fphe_ctx_limbs(const fphe_ctx* c, uint32_t* l2, uint32_t* l1) {
+  if (!c) return FPHE_ERR_ARG;
+  if (l2) *l2 = (uint32_t)c->L2;
+  if (l1) *l1 = (uint32_t)c->L1;
+  return FPHE_OK;
+}
+
+fphe_status fphe_encode_f32(const fphe_ctx* c, const float* x, size_t count, uint32_t* P, uint8_t* neg,
+                            int32_t* exp, int32_t* err, void* stream) {
+  if (!c || !err) return FPHE_ERR_ARG;
+  if (count == 0) return FPHE_OK;
+  if (!x || !P || !neg || !exp) return FPHE_ERR_ARG;
+  DevGuard g(c->device);
+  const unsigned grid = (unsigned)std::min<size_t>((count + 255) / 256, (size_t)c->cus * 8);
+  hipLaunchKernelGGL(k_encode_f32, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, count, P, neg, exp, err);
+  return hip_ok(hipGetLastError());
+}
+
+fphe_status fphe_encode_f64(const fphe_ctx* c, const double* x, size_t count, uint32_t* P, uint8_t* neg,
+                            int32_t* exp, int32_t* err, void* stream) {
+  if (!c || !err) return FPHE_ERR_ARG;
+  if (count == 0) return FPHE_OK;
+  if (!x || !P || !neg || !exp) return FPHE_ERR_ARG;
+  DevGuard g(c->device);
+  const unsigned grid = (unsigned)std::min<size_t>((count + 255) / 256, (size_t)c->cus * 8);
+  hipLaunchKernelGGL(k_encode_f64, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, count, P, neg, exp, err);
+  return hip_ok(hipGetLastError());
+}
+
+fphe_status fphe_decode_f32(const fphe_ctx* c, const uint32_t* P, uint32_t lp, const int32_t* exp, size_t count,
+                            float* out, int32_t* err, void* stream) {
+  if (!c || !err) return FPHE_ERR_ARG;
+  if (count == 0) return FPHE_OK;
+  if (!P || !exp || !out || lp == 0) return FPHE_ERR_ARG;
+  DevGuard g(c->device);
+  const unsigned grid = (unsigned)std::min<size_t>((count + 255) / 256, (size_t)c->cus * 8);
+  if (c->L1 == 64)
+    hipLaunchKernelGGL(k_decode_f32<64>, dim3(grid), dim3(256), 0, (hipStream_t)stream, c->K, P, lp, exp, count, out, err);
+  else
+    hipLaunchKernelGGL(k_decode_f32<32>, dim3(grid), dim3(256), 0, (hipStream_t)stream, c->K, P, lp, exp, count, out, err);
+  return hip_ok(hipGetLastError());
+}
+
+fphe_status fphe_decode_f64(const fphe_ctx* c, const uint32_t* P, uint32_t lp, const int32_t* exp, size_t count,
+                            double* out, int32_t* err, void* stream) {
+  if (!c || !err) return FPHE_ERR_ARG;
+  if (count == 0) return FPHE_OK;
+  if (!P || !exp || !out || lp == 0) return FPHE_ERR_ARG;
+  DevGuard g(c->device);
+  const unsigned grid = (unsigned)std::min<size_t>((count + 255) / 256, (size_t)c->cus * 8);
+  if (c->L1 == 64)
+    hipLaunchKernelGGL(k_decode_f64<64>, dim3(grid), dim3(256), 0, (hipStream_t)stream, c->K, P, lp, exp, count, out, err);
+  else
+    hipLaunchKernelGGL(k_decode_f64<32>, dim3(grid), dim3(256), 0, (hipStream_t)stream, c->K, P, lp, exp, count, out, err);
+  return hip_ok(hipGetLastError());
+}
+
+
+fphe_status fphe_encrypt(fphe_ctx* c, const uint32_t* P, uint32_t lp, const uint8_t* neg, size_t count, int obf,
+                         const uint32_t* r, const uint32_t rng_key[8], uint64_t nonce, uint32_t* C, uint8_t* sign,
+                         void* stream) {
+  if (!c) return FPHE_ERR_ARG;
+  if (count == 0) return FPHE_OK;
+  if (!P || !neg || !C || !sign || lp == 0 || lp > (uint32_t)c->L1) return FPHE_ERR_ARG;
+  if (count >= (1ull << 32)) return FPHE_ERR_ARG;
+  if (obf && !r && !rng_key) return FPHE_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DevGuard g(c->device);
+  if (c->L2 == 128) return launch_encrypt<128>(c, P, lp, neg, count, obf, r, rng_key, nonce, C, sign, (hipStream_t)stream);
+  return launch_encrypt<64>(c, P, lp, neg, count, obf, r, rng_key, nonce, C, sign, (hipStream_t)stream);
+}
+
+
+fphe_status fphe_decrypt(fphe_ctx* c, const uint32_t* C, size_t count, uint32_t* P, void* stream) {
+  if (!c) return FPHE_ERR_ARG;
+  if (!c->has_sk) return FPHE_ERR_NO_SK;
+  if (count == 0) return FPHE_OK;
+  if (!C || !P) return FPHE_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DevGuard g(c->device);
+  if (c->L2 == 128) return launch_decrypt<128>(c, C, count, P, (hipStream_t)stream);
+  return launch_decrypt<64>(c, C, count, P, (hipStream_t)stream);
+}
+
+
+fphe_status fphe_add(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, const int32_t* ea, const uint32_t* Cb,
+                     const uint8_t* sb, const int32_t* eb, int b_stride, size_t count, uint32_t* Co, uint8_t* so,
+                     int32_t* eo, void* stream) {
+  if (!c) return FPHE_ERR_ARG;
+  if (count == 0) return FPHE_OK;
+  if (!Ca || !sa || !ea || !Cb || !sb || !eb || !Co || !so || !eo) return FPHE_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DevGuard g(c->device);
+  if (c->L2 == 128) return launch_add<128>(c, Ca, sa, ea, Cb, sb, eb, b_stride, count, Co, so, eo, (hipStream_t)stream);
+  return launch_add<64>(c, Ca, sa, ea, Cb, sb, eb, b_stride, count, Co, so, eo, (hipStream_t)stream);
+}
+
+
+fphe_status fphe_mul(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, const int32_t* ea, const uint32_t* P,
+                     uint32_t lp, const uint8_t* pneg, const int32_t* pexp, int p_stride, size_t count, uint32_t* Co,
+                     uint8_t* so, int32_t* eo, int32_t* err, void* stream) {
+  if (!c || !err) return FPHE_ERR_ARG;
+  if (count == 0) return FPHE_OK;
+  if (!Ca || !sa || !ea || !P || !pneg || !pexp || !Co || !so || !eo || lp == 0) return FPHE_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DevGuard g(c->device);
+  if (c->L2 == 128)
+    return launch_mul<128>(c, Ca, sa, ea, P, lp, pneg, pexp, p_stride, count, Co, so, eo, err, (hipStream_t)stream);
+  return launch_mul<64>(c, Ca, sa, ea, P, lp, pneg, pexp, p_stride, count, Co, so, eo, err, (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,795 @@
+"""MI355X mirror of the reference's native surface ``fate_utils.paillier``.
+
+Reference: rust/fate_utils/crates/fate_utils/src/paillier/paillier.rs (pyo3 classes
+PK, SK, Coder, Ciphertext, CiphertextVector, PlaintextVector, Evaluator, keygen), backed
+by rust/fate_utils/crates/fixedpoint_paillier/src/lib.rs.
+
+Vectors live in GPU memory (HBM) in the tile-major SoA layout of include/fate_phe.h:
+limb j of element e is word ((e//64)*L + j)*64 + e%64 of a torch int32 tensor shaped
+[ntiles, L, 64].  Per-element sign (uint8) and exponent (int32) arrays are padded to
+ntiles*64.  All arithmetic runs in libfatephe.so; there is no CPU compute path --
+without a HIP device the constructors of device vectors raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import itertools
+import os
+import threading
+from typing import Dict, List, Optional, Sequence, Tuple, Union
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._keygen import keygen_primes
+
+WAVE = 64
+BASE = 16
+MAX_INT_FRACTION = 2
+
+
+class PanicException(BaseException):
+    """Raised where the reference Rust code panics (pyo3 surfaces those as
+    ``pyo3_runtime.PanicException``, a BaseException subclass)."""
+
+
+def _ntiles(n: int) -> int:
+    return (n + WAVE - 1) // WAVE
+
+
+def _device(device=None) -> torch.device:
+    if device is not None:
+        d = torch.device(device)
+        if d.type != "cuda":
+            raise ValueError("fate_amd vectors live on a HIP device (torch 'cuda')")
+        return d if d.index is not None else torch.device("cuda", torch.cuda.current_device())
+    if not torch.cuda.is_available():
+        raise RuntimeError("fate_amd requires a HIP device (torch.cuda.is_available() is False)")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def _stream(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+# --------------------------------------------------------------------------------------
+# host <-> tile-layout conversion (plumbing; not on the hot path)
+# --------------------------------------------------------------------------------------
+def ints_to_limbs(values: Sequence[int], limbs: int) -> np.ndarray:
+    """Non-negative ints -> uint32 [count, limbs] little-endian."""
+    nb = 4 * limbs
+    buf = b"".join(int(v).to_bytes(nb, "little") for v in values)
+    return np.frombuffer(buf, dtype=np.uint32).reshape(len(values), limbs) if values else \
+        np.zeros((0, limbs), dtype=np.uint32)
+
+
+def limbs_to_ints(arr: np.ndarray) -> List[int]:
+    """uint32 [count, limbs] -> Python ints."""
+    arr = np.ascontiguousarray(arr, dtype=np.uint32)
+    raw = arr.tobytes()
+    nb = arr.shape[1] * 4
+    return [int.from_bytes(raw[i * nb:(i + 1) * nb], "little") for i in range(arr.shape[0])]
+
+
+def rows_to_tiles(rows: np.ndarray) -> np.ndarray:
+    """uint32 [count, L] -> uint32 [ntiles, L, 64] (zero padded)."""
+    count, L = rows.shape
+    nt = _ntiles(count)
+    pad = np.zeros((nt * WAVE, L), dtype=np.uint32)
+    pad[:count] = rows
+    return np.ascontiguousarray(pad.reshape(nt, WAVE, L).transpose(0, 2, 1))
+
+
+def tiles_to_rows(tiles: np.ndarray, count: int) -> np.ndarray:
+    nt, L, _ = tiles.shape
+    return np.ascontiguousarray(tiles.transpose(0, 2, 1).reshape(nt * WAVE, L)[:count])
+
+
+def tiles_to_cols(t: torch.Tensor) -> torch.Tensor:
+    """[nt, L, 64] -> [L, nt*64] (element-major view, materialised)."""
+    nt, L, _ = t.shape
+    return t.permute(1, 0, 2).reshape(L, nt * WAVE)
+
+
+def cols_to_tiles(c: torch.Tensor) -> torch.Tensor:
+    L, n = c.shape
+    nt = _ntiles(n)
+    if n != nt * WAVE:
+        c = torch.cat([c, c.new_zeros((L, nt * WAVE - n))], dim=1)
+    return c.reshape(L, nt, WAVE).permute(1, 0, 2).contiguous()
+
+
+def _pad_flat(x: torch.Tensor, n: int) -> torch.Tensor:
+    nt = _ntiles(n)
+    if x.shape[0] == nt * WAVE:
+        return x.contiguous()
+    out = x.new_zeros(nt * WAVE)
+    out[: x.shape[0]] = x
+    return out
+
+
+# --------------------------------------------------------------------------------------
+# per-device key contexts
+# --------------------------------------------------------------------------------------
+class _KeyCtx:
+    """Owns one fphe_ctx per HIP device for a key (public, or public+private)."""
+
+    def __init__(self, n: int, p: Optional[int] = None, q: Optional[int] = None):
+        self.n, self.p, self.q = n, p, q
+        self.key_bits = n.bit_length()
+        if self.key_bits not in (1024, 2048):
+            raise ValueError(f"unsupported key size {self.key_bits} (1024 or 2048)")
+        self.L1 = self.key_bits // 32
+        self.L2 = 2 * self.L1
+        self._ctx: Dict[int, ctypes.c_void_p] = {}
+        self._lock = threading.Lock()
+        self.rng_key = (ctypes.c_uint32 * 8)(*np.frombuffer(os.urandom(32), dtype=np.uint32).tolist())
+        self._nonce = itertools.count(1)
+
+    def next_nonce(self) -> int:
+        return (os.getpid() << 40) ^ next(self._nonce)
+
+    def ctx(self, device: torch.device) -> ctypes.c_void_p:
+        idx = device.index
+        with self._lock:
+            c = self._ctx.get(idx)
+            if c is not None:
+                return c
+            lib = _lib.load()
+            nw = (ctypes.c_uint32 * self.L1)(*ints_to_limbs([self.n], self.L1)[0].tolist())
+            pw = qw = None
+            if self.p is not None:
+                lq = self.L1 // 2
+                pw = (ctypes.c_uint32 * lq)(*ints_to_limbs([self.p], lq)[0].tolist())
+                qw = (ctypes.c_uint32 * lq)(*ints_to_limbs([self.q], lq)[0].tolist())
+            out = ctypes.c_void_p()
+            _lib.check(lib.fphe_ctx_create(idx, self.key_bits, nw, pw, qw, ctypes.byref(out)), "fphe_ctx_create")
+            self._ctx[idx] = out
+            return out
+
+    def __del__(self):
+        try:
+            if self._ctx and _lib._lib is not None:
+                for c in self._ctx.values():
+                    _lib._lib.fphe_ctx_destroy(c)
+        except Exception:
+            pass
+
+
+_KEYS: Dict[Tuple[int, Optional[int]], _KeyCtx] = {}
+_KEYS_LOCK = threading.Lock()
+
+
+def _key_for(n: int, p: Optional[int] = None, q: Optional[int] = None) -> _KeyCtx:
+    """One device context per (key, public/private) per process, shared by PK/SK/Coder."""
+    with _KEYS_LOCK:
+        k = _KEYS.get((n, p))
+        if k is None:
+            k = _KEYS[(n, p)] = _KeyCtx(n, p, q)
+        return k
+
+
+def _fit_limbs(v: "CiphertextVector", L2: int) -> "CiphertextVector":
+    """Zero-extend / truncate limb rows to the key's L2 (exact for values < n^2; used for
+    ``zeros()`` vectors, which are created before the key is known)."""
+    if v.L2 == L2:
+        return v
+    if v.L2 > L2:
+        C = v.C[:, :L2, :].contiguous()
+    else:
+        C = torch.cat([v.C, v.C.new_zeros((v.C.shape[0], L2 - v.L2, WAVE))], dim=1)
+    return CiphertextVector(C, v.sign, v.exp, v.count)
+
+
+_ERR_MESSAGES = [
+    (_lib.EF_ENCODE_NONFINITE, "called `Option::unwrap()` on a `None` value"),
+    (_lib.EF_DECODE_CORRUPTED, "Attempted to decode corrupted number"),
+    (_lib.EF_DECODE_OVERFLOW, "Overflow detected in decrypted number"),
+    (_lib.EF_MUL_INVALID_PT, "invalid plaintext"),
+    (_lib.EF_NOT_INVERTIBLE, "called `Option::unwrap()` on a `None` value (non-invertible)"),
+]
+
+
+def _raise_err(err: torch.Tensor) -> None:
+    v = int(err.item())
+    if v:
+        for bit, msg in _ERR_MESSAGES:
+            if v & bit:
+                raise PanicException(msg)
+
+
+# --------------------------------------------------------------------------------------
+# vectors
+# --------------------------------------------------------------------------------------
+class PlaintextVector:
+    """Encoded plaintexts (``fixedpoint_paillier::PlaintextVector``, lib.rs:364-367):
+    significand magnitude limbs P [ntiles, lp, 64], negative flags, base-16 exponents."""
+
+    __slots__ = ("P", "neg", "exp", "count")
+
+    def __init__(self, P: torch.Tensor = None, neg: torch.Tensor = None, exp: torch.Tensor = None, count: int = 0):
+        self.P, self.neg, self.exp, self.count = P, neg, exp, count
+
+    @property
+    def lp(self) -> int:
+        return self.P.shape[1]
+
+    @property
+    def device(self) -> torch.device:
+        return self.P.device
+
+    def __len__(self) -> int:
+        return self.count
+
+    # host view -------------------------------------------------------------------
+    def to_ints(self) -> Tuple[List[int], List[int]]:
+        """(signed significands, exps) on the host."""
+        rows = tiles_to_rows(self.P.cpu().numpy().view(np.uint32), self.count)
+        mags = limbs_to_ints(rows)
+        neg = self.neg[: self.count].cpu().numpy()
+        sig = [-m if (g and m) else m for m, g in zip(mags, neg)]
+        return sig, self.exp[: self.count].cpu().tolist()
+
+    @staticmethod
+    def from_ints(sig: Sequence[int], exp: Sequence[int], device=None, lp: Optional[int] = None) -> "PlaintextVector":
+        dev = _device(device)
+        count = len(sig)
+        mags = [abs(int(s)) for s in sig]
+        need = max([1] + [(m.bit_length() + 31) // 32 for m in mags])
+        lp = max(lp or 0, need, 1)
+        tiles = rows_to_tiles(ints_to_limbs(mags, lp))
+        P = torch.from_numpy(tiles.view(np.int32)).to(dev)
+        neg = _pad_flat(torch.tensor([1 if s < 0 else 0 for s in sig], dtype=torch.uint8), count).to(dev)
+        ex = _pad_flat(torch.tensor(list(exp), dtype=torch.int32), count).to(dev)
+        return PlaintextVector(P, neg, ex, count)
+
+    def get_stride(self, index: int, stride: int) -> "PlaintextVector":
+        """``PlaintextVector.get_stride`` (paillier.rs:406-408; lib.rs:912-917)."""
+        return self._gather(torch.arange(index * stride, index * stride + stride, device=self.device))
+
+    def tolist(self) -> List["Plaintext"]:
+        return [Plaintext(self._gather(torch.tensor([i], device=self.device))) for i in range(self.count)]
+
+    def _gather(self, idx: torch.Tensor) -> "PlaintextVector":
+        cols = tiles_to_cols(self.P)[:, idx]
+        return PlaintextVector(cols_to_tiles(cols), _pad_flat(self.neg[idx], len(idx)),
+                               _pad_flat(self.exp[idx], len(idx)), len(idx))
+
+    def __str__(self):
+        return f"PlaintextVector(len={self.count}, lp={self.lp})"
+
+
+class Plaintext:
+    """Scalar plaintext (``fate_utils.paillier.Plaintext``): a length-1 vector."""
+
+    __slots__ = ("vec",)
+
+    def __init__(self, vec: PlaintextVector):
+        self.vec = vec
+
+
+class CiphertextVector:
+    """Encrypted vector (``fixedpoint_paillier::CiphertextVector``, lib.rs:353-356):
+    C [ntiles, L2, 64] canonical residues mod n^2, sign (reference integer = C - n^2),
+    exp (base-16 exponent)."""
+
+    __slots__ = ("C", "sign", "exp", "count")
+
+    def __init__(self, C: torch.Tensor = None, sign: torch.Tensor = None, exp: torch.Tensor = None, count: int = 0):
+        self.C, self.sign, self.exp, self.count = C, sign, exp, count
+
+    # ---- construction / host views -----------------------------------------------
+    @property
+    def device(self) -> torch.device:
+        return self.C.device
+
+    @property
+    def L2(self) -> int:
+        return self.C.shape[1]
+
+    def __len__(self) -> int:
+        return self.count
+
+    def __str__(self) -> str:
+        return f"CiphertextVector(len={self.count}, limbs={self.L2})"
+
+    __repr__ = __str__
+
+    @staticmethod
+    def empty(count: int, L2: int, device) -> "CiphertextVector":
+        nt = _ntiles(count)
+        return CiphertextVector(torch.empty((nt, L2, WAVE), dtype=torch.int32, device=device),
+                                torch.zeros(nt * WAVE, dtype=torch.uint8, device=device),
+                                torch.zeros(nt * WAVE, dtype=torch.int32, device=device), count)
+
+    @staticmethod
+    def zeros(size: int, L2: int = 128, device=None) -> "CiphertextVector":
+        """``CiphertextVector::zeros`` (lib.rs:434-437): literal 1 with exp 0 (:244-249)."""
+        dev = _device(device)
+        v = CiphertextVector.empty(size, L2, dev)
+        v.C.zero_()
+        v.C[:, 0, :] = 1
+        return v
+
+    def to_signed_ints(self, ns: int) -> Tuple[List[int], List[int]]:
+        """Reference (signed rug::Integer, exp) pairs, for parity checks and the wire."""
+        rows = tiles_to_rows(self.C.cpu().numpy().view(np.uint32), self.count)
+        mags = limbs_to_ints(rows)
+        sg = self.sign[: self.count].cpu().numpy()
+        out = [m - ns if (s and m) else m for m, s in zip(mags, sg)]
+        return out, self.exp[: self.count].cpu().tolist()
+
+    @staticmethod
+    def from_signed_ints(cs: Sequence[int], exps: Sequence[int], ns: int, L2: int, device=None) -> "CiphertextVector":
+        dev = _device(device)
+        count = len(cs)
+        canon = [c + ns if c < 0 else c for c in cs]
+        tiles = rows_to_tiles(ints_to_limbs(canon, L2))
+        C = torch.from_numpy(tiles.view(np.int32)).to(dev)
+        sign = _pad_flat(torch.tensor([1 if c < 0 else 0 for c in cs], dtype=torch.uint8), count).to(dev)
+        ex = _pad_flat(torch.tensor(list(exps), dtype=torch.int32), count).to(dev)
+        return CiphertextVector(C, sign, ex, count)
+
+    # ---- pickling (wire format of this backend) ---------------------
+    def __getstate__(self):
+        return {"C": self.C.cpu(), "sign": self.sign.cpu(), "exp": self.exp.cpu(), "count": self.count}
+
+    def __setstate__(self, st):
+        dev = _device()
+        self.C, self.sign, self.exp, self.count = st["C"].to(dev), st["sign"].to(dev), st["exp"].to(dev), st["count"]
+
+    # ---- element plumbing (torch indexing; no arithmetic) ---------------------------
+    def _gather(self, idx: torch.Tensor) -> "CiphertextVector":
+        idx = idx.to(self.device)
+        cols = tiles_to_cols(self.C)[:, idx]
+        return CiphertextVector(cols_to_tiles(cols), _pad_flat(self.sign[idx], len(idx)),
+                                _pad_flat(self.exp[idx], len(idx)), len(idx))
+
+    def _assign(self, idx: torch.Tensor, src: "CiphertextVector") -> None:
+        idx = idx.to(self.device)
+        cols = tiles_to_cols(self.C)
+        cols[:, idx] = tiles_to_cols(src.C)[:, : src.count]
+        self.C = cols_to_tiles(cols)[: self.C.shape[0]]
+        self.sign[idx] = src.sign[: src.count]
+        self.exp[idx] = src.exp[: src.count]
+
+    def slice(self, start: int, size: int) -> "CiphertextVector":
+        """``CiphertextVector::slice`` (lib.rs:452-455)."""
+        if start + size > self.count:
+            raise PanicException(f"range end index {start + size} out of range for slice of length {self.count}")
+        return self._gather(torch.arange(start, start + size))
+
+    def slice_indexes(self, indexes: Sequence[int]) -> "CiphertextVector":
+        """``CiphertextVector::slice_indexes`` (lib.rs:457-463)."""
+        return self._gather(torch.as_tensor(list(indexes), dtype=torch.long))
+
+    def cat(self, others: Sequence["CiphertextVector"]) -> "CiphertextVector":
+        """``CiphertextVector::cat`` (lib.rs:465-471)."""
+        return Evaluator.cat([self, *others])
+
+    def shuffle(self, indexes: Sequence[int]) -> "CiphertextVector":
+        """``CiphertextVector::shuffle`` (lib.rs:492-497): result[i] = data[indexes[i]] for a
+        permutation, realised as a gather (same result as the reference's cycle walk)."""
+        out = CiphertextVector(self.C.clone(), self.sign.clone(), self.exp.clone(), self.count)
+        out.i_shuffle(indexes)
+        return out
+
+    def i_shuffle(self, indexes: Sequence[int]) -> None:
+        """``CiphertextVector::i_shuffle`` (lib.rs:473-490).  The cycle walk permutes
+        data so that new[i] = old[indexes[i]] when ``indexes`` is a permutation."""
+        idx = torch.as_tensor(list(indexes), dtype=torch.long)
+        g = self._gather(idx)
+        self.C, self.sign, self.exp = g.C, g.sign, g.exp
+
+    def intervals_slice(self, intervals: Sequence[Tuple[int, int]]) -> "CiphertextVector":
+        """``CiphertextVector::intervals_slice`` (lib.rs:499-513)."""
+        parts = []
+        for s, e in intervals:
+            if e > self.count:
+                raise RuntimeError(f"end index out of range: start={s}, end={e}, data_size={self.count}")
+            parts.append(torch.arange(s, e))
+        idx = torch.cat(parts) if parts else torch.zeros(0, dtype=torch.long)
+        return self._gather(idx)
+
+    def tolist(self) -> List["CiphertextVector"]:
+        return [self._gather(torch.tensor([i])) for i in range(self.count)]
+
+    # ---- arithmetic (device kernels) ----------------------------------------------
+    def add(self, pk: "PK", other: "CiphertextVector") -> "CiphertextVector":
+        """``CiphertextVector::add`` (lib.rs:797-805)."""
+        return _add(pk, self, other, broadcast=False)
+
+    def add_scalar(self, pk: "PK", other: "Ciphertext") -> "CiphertextVector":
+        """``CiphertextVector::add_scalar`` (lib.rs:807-810)."""
+        return _add(pk, self, other.vec, broadcast=True)
+
+    def iadd(self, pk: "PK", other: "CiphertextVector") -> None:
+        """``CiphertextVector::iadd`` (lib.rs:748-752)."""
+        r = _add(pk, self, other, broadcast=False, count=min(self.count, other.count))
+        self._overwrite_prefix(r)
+
+    def idouble(self, pk: "PK") -> None:
+        """``CiphertextVector::idouble`` (lib.rs:753-758): x.add(x)."""
+        r = _add(pk, self, self, broadcast=False)
+        self.C, self.sign, self.exp = r.C, r.sign, r.exp
+
+    def iadd_vec(self, other: "CiphertextVector", sa: int, sb: int, size: Optional[int], pk: "PK") -> None:
+        """``CiphertextVector::iadd_vec`` (lib.rs:634-677)."""
+        if size is None:
+            size = min(self.count - sa, other.count - sb)
+        else:
+            if sa + size > self.count:
+                raise RuntimeError(f"end index out of range: sa={sa}, ea={sa + size}, data_size={self.count}")
+            if sb + size > other.count:
+                raise RuntimeError(f"end index out of range: sb={sb}, eb={sb + size}, data_size={other.count}")
+        if size <= 0:
+            return
+        a = self.slice(sa, size)
+        b = other.slice(sb, size)
+        self._assign(torch.arange(sa, sa + size), _add(pk, a, b, broadcast=False))
+
+    def mul(self, pk: "PK", other: PlaintextVector) -> "CiphertextVector":
+        """``CiphertextVector::mul`` (lib.rs:842-850)."""
+        return _mul(pk, self, other, broadcast=False)
+
+    def mul_scalar(self, pk: "PK", other: Plaintext) -> "CiphertextVector":
+        """``CiphertextVector::mul_scalar`` (lib.rs:852-859)."""
+        return _mul(pk, self, other.vec, broadcast=True)
+
+    def _overwrite_prefix(self, r: "CiphertextVector") -> None:
+        if r.count == self.count:
+            self.C, self.sign, self.exp = r.C, r.sign, r.exp
+        else:
+            self._assign(torch.arange(0, r.count), r)
+
+
+class Ciphertext:
+    """Scalar ciphertext (``fate_utils.paillier.Ciphertext``): a length-1 vector."""
+
+    __slots__ = ("vec",)
+
+    def __init__(self, vec: CiphertextVector):
+        self.vec = vec
+
+
+# --------------------------------------------------------------------------------------
+# kernel launchers
+# --------------------------------------------------------------------------------------
+def _add(pk: "PK", a: CiphertextVector, b: CiphertextVector, broadcast: bool, count: Optional[int] = None
+         ) -> CiphertextVector:
+    dev = a.device
+    a, b = _fit_limbs(a, pk._key.L2), _fit_limbs(b, pk._key.L2)
+    n = a.count if count is None else count
+    if not broadcast and b.count < n:
+        n = b.count  # zip() semantics of the reference (lib.rs:797-805)
+    out = CiphertextVector.empty(n, a.L2, dev)
+    if n == 0:
+        return out
+    lib = _lib.load()
+    ctx = pk._key.ctx(dev)
+    _lib.check(lib.fphe_add(ctx, _ptr(a.C), _ptr(a.sign), _ptr(a.exp), _ptr(b.C), _ptr(b.sign), _ptr(b.exp),
+                            0 if broadcast else 1, n, _ptr(out.C), _ptr(out.sign), _ptr(out.exp),
+                            ctypes.c_void_p(_stream(dev))), "fphe_add")
+    return out
+
+
+def _mul(pk: "PK", a: CiphertextVector, p: PlaintextVector, broadcast: bool) -> CiphertextVector:
+    dev = a.device
+    a = _fit_limbs(a, pk._key.L2)
+    n = a.count if broadcast else min(a.count, p.count)
+    out = CiphertextVector.empty(n, a.L2, dev)
+    if n == 0:
+        return out
+    lib = _lib.load()
+    ctx = pk._key.ctx(dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    P = p.P if p.lp <= pk._key.L1 else p.P[:, : pk._key.L1].contiguous()
+    _lib.check(lib.fphe_mul(ctx, _ptr(a.C), _ptr(a.sign), _ptr(a.exp), _ptr(P), P.shape[1], _ptr(p.neg),
+                            _ptr(p.exp), 0 if broadcast else 1, n, _ptr(out.C), _ptr(out.sign), _ptr(out.exp),
+                            _ptr(err), ctypes.c_void_p(_stream(dev))), "fphe_mul")
+    v = int(err.item())
+    if v & _lib.EF_MUL_INVALID_PT:
+        raise PanicException("invalid plaintext")
+    if v & _lib.EF_NOT_INVERTIBLE:
+        raise NotImplementedError("ct x negative plaintext needs a modular inverse: not yet implemented on device")
+    return out
+
+
+# --------------------------------------------------------------------------------------
+# keys and coder
+# --------------------------------------------------------------------------------------
+class PK:
+    """``fate_utils.paillier.PK`` (paillier.rs:50-75; fixedpoint_paillier::PK lib.rs:18-34)."""
+
+    def __init__(self, n: Optional[int] = None):
+        self.n = n
+        if n is not None:
+            self._init(n)
+
+    def _init(self, n: int):
+        self.n = n
+        self.ns = n * n
+        self.max_int = n // MAX_INT_FRACTION
+        self._key = _key_for(n)
+
+    def encrypt_encoded(self, plaintext_vector: PlaintextVector, obfuscate: bool,
+                        r: Optional[Sequence[int]] = None) -> CiphertextVector:
+        """``PK.encrypt_encoded`` (paillier.rs:51-57 -> lib.rs:370-381).  ``r`` (our extension)
+        injects the obfuscation nonces (parity mode); default draws them on the device."""
+        pv = plaintext_vector
+        dev = pv.device
+        k = self._key
+        n = pv.count
+        out = CiphertextVector.empty(n, k.L2, dev)
+        if n == 0:
+            return out
+        if pv.lp > k.L1:
+            raise PanicException("plaintext does not fit the key")
+        rt = None
+        if r is not None:
+            if len(r) != n:
+                raise ValueError("need one r per element")
+            rt = torch.from_numpy(rows_to_tiles(ints_to_limbs(list(r), k.L1)).view(np.int32)).to(dev)
+        lib = _lib.load()
+        _lib.check(lib.fphe_encrypt(k.ctx(dev), _ptr(pv.P), pv.lp, _ptr(pv.neg), n, 1 if obfuscate else 0,
+                                    _ptr(rt), k.rng_key, k.next_nonce(), _ptr(out.C), _ptr(out.sign),
+                                    ctypes.c_void_p(_stream(dev))), "fphe_encrypt")
+        out.exp[:n] = pv.exp[:n]
+        return out
+
+    def encrypt_encoded_scalar(self, plaintext: Plaintext, obfuscate: bool) -> Ciphertext:
+        """``PK.encrypt_encoded_scalar`` (paillier.rs:58-60)."""
+        return Ciphertext(self.encrypt_encoded(plaintext.vec, obfuscate))
+
+    def __getstate__(self):
+        return {"n": self.n}
+
+    def __setstate__(self, st):
+        self._init(st["n"])
+
+
+class SK:
+    """``fate_utils.paillier.SK`` (paillier.rs:77-99; paillier::SK lib.rs:55-69, 124-177)."""
+
+    def __init__(self, p: Optional[int] = None, q: Optional[int] = None):
+        if p is not None:
+            self._init(p, q)
+
+    def _init(self, p: int, q: int):
+        if p == q:
+            raise PanicException("p == q")
+        self.p, self.q = (p, q) if p < q else (q, p)
+        self.n = self.p * self.q
+        self._key = _key_for(self.n, self.p, self.q)
+
+    def decrypt_to_encoded(self, data: CiphertextVector) -> PlaintextVector:
+        """``SK.decrypt_to_encoded`` (paillier.rs:79-81 -> lib.rs:392-399)."""
+        dev = data.device
+        k = self._key
+        data = _fit_limbs(data, k.L2)
+        n = data.count
+        nt = _ntiles(n)
+        P = torch.empty((nt, k.L1, WAVE), dtype=torch.int32, device=dev)
+        out = PlaintextVector(P, torch.zeros(nt * WAVE, dtype=torch.uint8, device=dev),
+                              data.exp.clone(), n)
+        if n == 0:
+            return out
+        lib = _lib.load()
+        _lib.check(lib.fphe_decrypt(k.ctx(dev), _ptr(data.C), n, _ptr(P), ctypes.c_void_p(_stream(dev))),
+                   "fphe_decrypt")
+        return out
+
+    def decrypt_to_encoded_scalar(self, data: Ciphertext) -> Plaintext:
+        return Plaintext(self.decrypt_to_encoded(data.vec))
+
+    def __getstate__(self):
+        return {"p": self.p, "q": self.q}
+
+    def __setstate__(self, st):
+        self._init(st["p"], st["q"])
+
+
+class Coder:
+    """``fate_utils.paillier.Coder`` (paillier.rs:101-204; fixedpoint_paillier::Coder lib.rs:53-193)."""
+
+    def __init__(self, n: Optional[int] = None):
+        if n is not None:
+            self._init(n)
+
+    def _init(self, n: int):
+        self.n = n
+        self.max_int = n // MAX_INT_FRACTION
+        self._key = _key_for(n)
+
+    def __getstate__(self):
+        return {"n": self.n}
+
+    def __setstate__(self, st):
+        self._init(st["n"])
+
+    # ---- vector encode (device) ------------------------------------------------------
+    def _encode_float(self, arr, dtype: torch.dtype, device=None) -> PlaintextVector:
+        dev = _device(device if device is not None else (arr.device if isinstance(arr, torch.Tensor)
+                                                         and arr.is_cuda else None))
+        x = torch.as_tensor(arr).detach().flatten().to(dtype=dtype, device=dev).contiguous()
+        n = x.numel()
+        nt = _ntiles(n)
+        P = torch.zeros((nt, 2, WAVE), dtype=torch.int32, device=dev)
+        neg = torch.zeros(nt * WAVE, dtype=torch.uint8, device=dev)
+        ex = torch.zeros(nt * WAVE, dtype=torch.int32, device=dev)
+        out = PlaintextVector(P, neg, ex, n)
+        if n == 0:
+            return out
+        err = torch.zeros(1, dtype=torch.int32, device=dev)
+        lib = _lib.load()
+        fn = lib.fphe_encode_f32 if dtype == torch.float32 else lib.fphe_encode_f64
+        _lib.check(fn(self._key.ctx(dev), _ptr(x), n, _ptr(P), _ptr(neg), _ptr(ex), _ptr(err),
+                      ctypes.c_void_p(_stream(dev))), "fphe_encode")
+        _raise_err(err)
+        return out
+
+    def encode_f32_vec(self, data, device=None) -> PlaintextVector:
+        """``Coder.encode_f32_vec`` (paillier.rs:162-169)."""
+        return self._encode_float(data, torch.float32, device)
+
+    def encode_f64_vec(self, data, device=None) -> PlaintextVector:
+        """``Coder.encode_f64_vec`` (paillier.rs:145-152)."""
+        return self._encode_float(data, torch.float64, device)
+
+    def _encode_int(self, data, device=None) -> PlaintextVector:
+        # encode_i64 / encode_i32 (lib.rs:68-78, 119-129): sig = v (v >= 0) or n + v, exp 0
+        dev = _device(device if device is not None else (data.device if isinstance(data, torch.Tensor)
+                                                         and data.is_cuda else None))
+        v = np.asarray(torch.as_tensor(data).detach().flatten().cpu().numpy(), dtype=np.int64)
+        n = v.size
+        L1 = self._key.L1
+        rows = np.zeros((n, L1), dtype=np.uint32)
+        nonneg = v >= 0
+        pos = v.astype(np.uint64)
+        rows[nonneg, 0] = (pos[nonneg] & 0xFFFFFFFF).astype(np.uint32)
+        rows[nonneg, 1] = (pos[nonneg] >> np.uint64(32)).astype(np.uint32)
+        negidx = np.nonzero(~nonneg)[0]
+        if negidx.size:
+            mag = (-(v[negidx].astype(object))).astype(object)
+            nl = ints_to_limbs([self.n], L1)[0].astype(np.int64)
+            m = np.array([int(x) for x in mag], dtype=object)
+            sub = np.zeros((negidx.size, L1), dtype=np.int64)
+            sub[:, 0] = np.array([int(x) & 0xFFFFFFFF for x in m], dtype=np.int64)
+            sub[:, 1] = np.array([int(x) >> 32 for x in m], dtype=np.int64)
+            br = np.zeros(negidx.size, dtype=np.int64)
+            res = np.zeros((negidx.size, L1), dtype=np.uint32)
+            for j in range(L1):
+                d = nl[j] - sub[:, j] - br
+                br = (d < 0).astype(np.int64)
+                res[:, j] = (d + (br << 32)).astype(np.uint32)
+            rows[negidx] = res
+        P = torch.from_numpy(rows_to_tiles(rows).view(np.int32)).to(dev)
+        nt = _ntiles(n)
+        return PlaintextVector(P, torch.zeros(nt * WAVE, dtype=torch.uint8, device=dev),
+                               torch.zeros(nt * WAVE, dtype=torch.int32, device=dev), n)
+
+    def encode_i64_vec(self, data, device=None) -> PlaintextVector:
+        """``Coder.encode_i64_vec`` (paillier.rs:182-189)."""
+        return self._encode_int(data, device)
+
+    def encode_i32_vec(self, data, device=None) -> PlaintextVector:
+        """``Coder.encode_i32_vec`` (paillier.rs:193-200)."""
+        return self._encode_int(data, device)
+
+    # ---- vector decode (device) -------------------------------------------------------
+    def _decode_float(self, data: PlaintextVector, dtype: torch.dtype) -> torch.Tensor:
+        dev = data.device
+        n = data.count
+        out = torch.empty(n, dtype=dtype, device=dev)
+        if n == 0:
+            return out
+        err = torch.zeros(1, dtype=torch.int32, device=dev)
+        lib = _lib.load()
+        fn = lib.fphe_decode_f32 if dtype == torch.float32 else lib.fphe_decode_f64
+        P = data.P
+        _lib.check(fn(self._key.ctx(dev), _ptr(P), P.shape[1], _ptr(data.exp), n, _ptr(out), _ptr(err),
+                      ctypes.c_void_p(_stream(dev))), "fphe_decode")
+        _raise_err(err)
+        return out
+
+    def decode_f32_vec(self, data: PlaintextVector) -> torch.Tensor:
+        """``Coder.decode_f32_vec`` (paillier.rs:173-181); returns a device tensor."""
+        return self._decode_float(data, torch.float32)
+
+    def decode_f64_vec(self, data: PlaintextVector) -> torch.Tensor:
+        """``Coder.decode_f64_vec`` (paillier.rs:153-161); returns a device tensor."""
+        return self._decode_float(data, torch.float64)
+
+    def _mantissa(self, sig: int) -> int:
+        if sig > self.n:
+            raise PanicException("Attempted to decode corrupted number")
+        if sig <= self.max_int:
+            return sig
+        if sig >= self.n - self.max_int:
+            return sig - self.n
+        raise PanicException("Overflow detected in decrypted number")
+
+    def decode_i64_vec(self, data: PlaintextVector) -> List[int]:
+        """``Coder.decode_i64_vec`` (paillier.rs:190-192; decode_i64 lib.rs:130-142)."""
+        sig, exps = data.to_ints()
+        out = []
+        for s, e in zip(sig, exps):
+            m = self._mantissa(s)
+            v = m << (4 * e) if e >= 0 else m >> (-4 * e)
+            if not -(1 << 127) <= v < (1 << 127):
+                raise PanicException("cant't convert to i128")
+            v &= (1 << 64) - 1
+            out.append(v - (1 << 64) if v >= (1 << 63) else v)
+        return out
+
+    def decode_i32_vec(self, data: PlaintextVector) -> List[int]:
+        """``Coder.decode_i32_vec``: decode_f64 as i32 (saturating cast, lib.rs:143-146)."""
+        f = self.decode_f64_vec(data).cpu().tolist()
+        out = []
+        for x in f:
+            if x != x:
+                out.append(0)
+            else:
+                out.append(int(max(-(2 ** 31), min(2 ** 31 - 1, int(x) if abs(x) < 2 ** 63 else
+                                                   (2 ** 31 if x > 0 else -(2 ** 31))))))
+        return out
+
+    # ---- scalars (length-1 vectors) ---------------------------------------------------
+    def encode_f64(self, data: float) -> Plaintext:
+        return Plaintext(self.encode_f64_vec(torch.tensor([data], dtype=torch.float64)))
+
+    def encode_f32(self, data: float) -> Plaintext:
+        return Plaintext(self.encode_f32_vec(torch.tensor([data], dtype=torch.float32)))
+
+    def encode_i64(self, data: int) -> Plaintext:
+        return Plaintext(self.encode_i64_vec(torch.tensor([data], dtype=torch.int64)))
+
+    def encode_i32(self, data: int) -> Plaintext:
+        return Plaintext(self.encode_i32_vec(torch.tensor([data], dtype=torch.int64)))
+
+    def decode_f64(self, data: Plaintext) -> float:
+        return float(self.decode_f64_vec(data.vec)[0].item())
+
+    def decode_f32(self, data: Plaintext) -> float:
+        return float(self.decode_f32_vec(data.vec)[0].item())
+
+    def decode_i64(self, data: Plaintext) -> int:
+        return self.decode_i64_vec(data.vec)[0]
+
+    def decode_i32(self, data: Plaintext) -> int:
+        return self.decode_i32_vec(data.vec)[0]
+
+
+class Evaluator:
+    """``fate_utils.paillier.Evaluator`` (paillier.rs:414-432)."""
+
+    @staticmethod
+    def cat(vec_list: Sequence[CiphertextVector]) -> CiphertextVector:
+        vecs = [v for v in vec_list if v.count > 0]
+        if not vecs:
+            return CiphertextVector.zeros(0, vec_list[0].L2 if vec_list else 128)
+        cols = torch.cat([tiles_to_cols(v.C)[:, : v.count] for v in vecs], dim=1)
+        n = cols.shape[1]
+        return CiphertextVector(cols_to_tiles(cols),
+                                _pad_flat(torch.cat([v.sign[: v.count] for v in vecs]), n),
+                                _pad_flat(torch.cat([v.exp[: v.count] for v in vecs]), n), n)
+
+    @staticmethod
+    def slice_indexes(a: CiphertextVector, indexes: Sequence[int]) -> CiphertextVector:
+        return a.slice_indexes(indexes)
+
+
+def keygen(bit_length: int) -> Tuple[SK, PK, Coder]:
+    """``fate_utils.paillier.keygen`` (paillier.rs:206-210; fixedpoint_paillier::keygen lib.rs:408-413)."""
+    p, q = keygen_primes(bit_length)
+    return SK(p, q), PK(p * q), Coder(p * q)
+
+
+def keypair_from_primes(p: int, q: int) -> Tuple[SK, PK, Coder]:
+    """Deterministic key construction for tests / fixtures."""
+    return SK(p, q), PK(p * q), Coder(p * q)
