@@ -1,0 +1,241 @@
+#!/usr/bin/env python3
+"""bench.py -- Paillier-2048 encrypt throughput, device-resident (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): 2048-bit key, float32 tensor of 2^20 elements per GPU
+(x = randn*4, seed 20241218+rank, first 8 entries [0,-0,1e-30,-1e-30,3.4e38,-3.4e38,1,-1]),
+already resident in HBM.  One step = fixed-point encode (device) + obfuscated encryption
+(device ChaCha20 r, r^n mod n^2) of the whole batch.  N GPUs = N independent shards (weak
+scaling, one process per GPU, no collective in the timed region).  Also reported (N=1 leg
+and every rank): decrypt and ct-add throughput on the same data, the end-to-end rate with
+host->device and device->host copies, a decrypt round-trip check, the roofline of the
+dominant kernel and the CPU baseline (libgmp port of the reference call sequence).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n ELEMENTS]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+KEY_FIXTURE = os.path.join(ROOT, "tests", "golden", "paillier_2048.json")
+# gfx950 integer MAC peak: 256 CU x 128 lanes/clk x 2.4 GHz at v_mad_u64_u32's half rate
+# (measured half rate in profiles/r01_probe_alu.txt); one MAC32 = 32x32->64 multiply-add.
+PEAK_TMAC32 = 256 * 128 * 2.4e9 / 2 / 1e12
+PEAK_HBM_GBS = 8000.0
+
+
+def mac32_per_mont(L: int) -> int:
+    return 2 * L * L + L
+
+
+def enc_mac32_per_elem(key_bits: int) -> float:
+    # fixed-window (w=5) modexp with an E-bit exponent = E + ceil(E/5) + 16
+    # Montgomery products, + 1 for the nude-ciphertext product; L = limbs of n^2.
+    E = key_bits
+    L = key_bits // 16
+    return (E + math.ceil(E / 5) + 16 + 1) * mac32_per_mont(L)
+
+
+def dec_mac32_per_elem(key_bits: int) -> float:
+    E = key_bits // 2
+    L = key_bits // 32
+    return 2 * (E + math.ceil(E / 5) + 16) * mac32_per_mont(L)
+
+
+def cpu_baseline(p: int, q: int, seconds: float = 12.0):
+    """libgmp restatement of the reference's per-element encrypt (oracle/gmp_ref.c)."""
+    from oracle import gmp_ref
+    key = gmp_ref.GmpKey(p * q, p, q)
+    t1 = key.bench("encrypt", 20, 1)
+    per1 = 20 / t1
+    threads = int(os.environ.get("FPHE_CPU_THREADS", "16"))
+    per_thread = max(8, int(per1 * seconds))
+    tw = key.bench("encrypt", per_thread, threads)
+    return {
+        "value": round(per_thread * threads / tw, 2),
+        "unit": "encrypts/s",
+        "cores": threads,
+        "kind": "port",
+        "per_core": round(per1, 2),
+        "sample": f"{per_thread * threads} Paillier-2048 obfuscated encryptions ({per_thread}/thread x {threads} "
+                  f"pthreads) through libgmp mpz_powm/mul/tdiv_r in the reference's call order (oracle/gmp_ref.c)",
+    }
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--n", type=int, default=1 << 20, help="elements per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip decrypt/add/e2e legs")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from fate_amd import paillier as P
+
+    with open(KEY_FIXTURE) as f:
+        fx = json.load(f)
+    p, q = int(fx["p"], 16), int(fx["q"], 16)
+    sk, pk, coder = P.keypair_from_primes(p, q)
+    key_bits = pk.n.bit_length()
+
+    N = args.n
+    g = torch.Generator().manual_seed(20241218 + rank)
+    x = torch.randn(N, generator=g, dtype=torch.float32) * 4
+    x[:8] = torch.tensor([0.0, -0.0, 1e-30, -1e-30, 3.4e38, -3.4e38, 1.0, -1.0])
+    xd = x.to(dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def barrier():
+        torch.cuda.synchronize(dev)
+        if dist:
+            tdist.barrier()
+
+    def step():
+        pv = coder.encode_f32_vec(xd)
+        return pk.encrypt_encoded(pv, True)
+
+    # warmup (also allocates the modexp scratch)
+    ct = None
+    for _ in range(max(args.warmup, 0)):
+        ct = step()
+    barrier()
+
+    # timed region; HIP events on the stream the kernels are launched on
+    ev_enc = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pv = coder.encode_f32_vec(xd)
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        ct = pk.encrypt_encoded(pv, True)
+        e1.record(stream)
+        ev_enc.append((e0, e1))
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    enc_kernel_ms = sum(a.elapsed_time(b) for a, b in ev_enc) / max(len(ev_enc), 1)
+    value = world * N * args.steps / elapsed
+
+    extras = {}
+    if not args.no_extras:
+        # decrypt (device-resident), with the bit-exact round trip check
+        torch.cuda.synchronize(dev)
+        e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        pt = sk.decrypt_to_encoded(ct)
+        e1.record(stream)
+        y = coder.decode_f32_vec(pt)
+        torch.cuda.synchronize(dev)
+        dec_ms = e0.elapsed_time(e1)
+        xb = x.numpy().view(np.uint32).copy()
+        xb[xb == 0x80000000] = 0  # -0.0 encodes to significand 0 -> decodes +0.0 (reference)
+        roundtrip_ok = bool(np.array_equal(y.cpu().numpy().view(np.uint32), xb))
+        # ct-add (Hetero-LR aggregate shape): enc(x) + enc(0.25*x') elementwise, exps differ
+        ct2 = pk.encrypt_encoded(coder.encode_f32_vec(torch.flip(xd, [0]) * 0.25), True)
+        torch.cuda.synchronize(dev)
+        e0.record(stream)
+        s = ct.add(pk, ct2)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        add_ms = e0.elapsed_time(e1)
+        # end-to-end from host f32 to host ciphertexts (pinned), one pass
+        xh = x.pin_memory()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        ce = pk.encrypt_encoded(coder.encode_f32_vec(xh.to(dev, non_blocking=True)), True)
+        Ch = torch.empty(ce.C.shape, dtype=ce.C.dtype, pin_memory=True)
+        Ch.copy_(ce.C, non_blocking=True)
+        sh = ce.sign.cpu(); eh = ce.exp.cpu()
+        torch.cuda.synchronize(dev)
+        e2e = time.perf_counter() - t0
+        extras = {
+            "decrypt_per_s": round(N / (dec_ms / 1e3), 1),
+            "ct_add_per_s": round(N / (add_ms / 1e3), 1),
+            "e2e_host_encrypts_per_s": round(N / e2e, 1),
+            "roundtrip_bit_exact": roundtrip_ok,
+            "decrypt_roofline_frac": round(N * dec_mac32_per_elem(key_bits) / (dec_ms / 1e3) / 1e12 / PEAK_TMAC32, 4),
+        }
+        del pt, y, ct2, s, ce, Ch
+
+    if rank != 0:
+        if dist:
+            tdist.barrier()
+            tdist.destroy_process_group()
+        return
+
+    mac_launch = N * enc_mac32_per_elem(key_bits)
+    achieved = mac_launch / (enc_kernel_ms / 1e3) / 1e12
+    # algorithmic HBM bytes per element: f32 sig/exp/neg read (13 B) + C (512 B) + sign (1 B) written
+    hbm_bytes = N * (8 + 1 + 4 + key_bits // 4 + 1)
+    roofline = {
+        "bound": "valu",
+        "kernel": "k_encrypt<128,5>",
+        "achieved": round(achieved, 3),
+        "peak": round(PEAK_TMAC32, 3),
+        "unit": "TMAC32/s",
+        "frac": round(achieved / PEAK_TMAC32, 4),
+        "traffic": None,
+        "per_elem_mac32": enc_mac32_per_elem(key_bits),
+        "kernel_ms": round(enc_kernel_ms, 3),
+        "hbm": {"achieved": round(hbm_bytes / (enc_kernel_ms / 1e3) / 1e9, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s"},
+    }
+    out = {
+        "metric": "Paillier-2048 encrypts/sec device-resident",
+        "value": round(value, 1),
+        "unit": "encrypts/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic",
+        "config": {"workload": "paillier2048_encrypt_f32_1M", "key_bits": key_bits, "elements_per_gpu": N,
+                   "obfuscate": True, "parallelism": f"shard{world}"},
+        "roofline": roofline,
+    }
+    out.update(extras)
+    if world == 1 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(p, q)
+        except Exception as exc:  # GMP missing on the box: say so, do not fake a number
+            out["cpu_baseline"] = {"value": None, "unit": "encrypts/s", "cores": 0, "kind": "port",
+                                   "sample": f"unavailable: {exc}"}
+    print(json.dumps(out))
+    if dist:
+        tdist.barrier()
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
