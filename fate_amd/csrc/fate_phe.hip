@@ -12,6 +12,7 @@
 
 #include "../../include/fate_phe.h"
 #include "mont_dev.h"
+#include "mont2_dev.h"
 #include "chacha_dev.h"
 #include "host_bn.h"
 
@@ -47,6 +48,11 @@ __device__ __forceinline__ void set_err(int32_t* err, u32 f) {
   if (f) atomicOr(err, (int32_t)f);
 }
 
+// word index of limb j of element e in a tile-major [ntiles][lp][64] vector
+__device__ __forceinline__ size_t tiled(size_t e, u32 lp, u32 j) {
+  return ((e >> 6) * lp + j) * FPHE_WAVE + (e & 63);
+}
+
 // Per-kernel geometry: one 64-element tile per wave per grid-stride step.
 struct WaveCtx {
   int lane;
@@ -74,11 +80,13 @@ __device__ __forceinline__ u32* lds_slot(u32* lds, int lane) {
 //   mod n^2 (the invert branch computes inv(1 - (n-m)n) = 1 + m n), and the sign of
 //   the truncating product at :116 is the sign of m (r^n > 0).
 // ======================================================================================
-template <int L>
+// C_nude = 1 + m*n (m >= 0) or n^2 - |m| n + 1 (m < 0) into an LDS column with limb
+// stride S (64 for one lane per element, 32 for two).
+template <int L, int S = FPHE_WAVE>
 __device__ __forceinline__ bool nude_to_slot(u32* slot, const KeyArgs& K, const Tile& Pt, u32 lp, bool negflag) {
   constexpr int L1 = L / 2;
 #pragma unroll
-  for (int j = 0; j < L; ++j) slot[j * FPHE_WAVE] = 0u;
+  for (int j = 0; j < L; ++j) slot[j * S] = 0u;
   u32 any = 0;
 #pragma unroll 1
   for (u32 k = 0; k < lp; ++k) {
@@ -87,18 +95,18 @@ __device__ __forceinline__ bool nude_to_slot(u32* slot, const KeyArgs& K, const 
     u64 acc = 0;
 #pragma unroll
     for (int j = 0; j < L1; ++j) {
-      u32* s = slot + (k + j) * FPHE_WAVE;
+      u32* s = slot + (k + j) * S;
       acc = (u64)pk * K.n[j] + *s + (acc >> 32);
       *s = (u32)acc;
     }
-    slot[(k + L1) * FPHE_WAVE] = (u32)(acc >> 32);
+    slot[(k + L1) * S] = (u32)(acc >> 32);
   }
   const bool mneg = negflag && (any != 0);
   if (mneg) {  // n^2 - |m| n
     u32 br = 0;
 #pragma unroll
     for (int j = 0; j < L; ++j) {
-      u32* s = slot + j * FPHE_WAVE;
+      u32* s = slot + j * S;
       const u64 d = (u64)K.N2[j] - *s - br;
       *s = (u32)d;
       br = (u32)(d >> 63);
@@ -107,7 +115,7 @@ __device__ __forceinline__ bool nude_to_slot(u32* slot, const KeyArgs& K, const 
   u32 c = 1;  // + 1
 #pragma unroll
   for (int j = 0; j < L; ++j) {
-    u32* s = slot + j * FPHE_WAVE;
+    u32* s = slot + j * S;
     const u64 t = (u64)*s + c;
     *s = (u32)t;
     c = (u32)(t >> 32);
@@ -115,14 +123,12 @@ __device__ __forceinline__ bool nude_to_slot(u32* slot, const KeyArgs& K, const 
   return mneg;
 }
 
-template <int L>
-__device__ __forceinline__ void draw_r(u32 (&A)[L], const KeyArgs& K, const ChaChaKey& ck, u64 nonce, size_t e) {
-  constexpr int L1 = L / 2;
+// r uniform in [1, n-1] (L1 = limbs of n) from this element's ChaCha20 stream.
+template <int L1>
+__device__ __forceinline__ void draw_r(u32 (&A)[L1], const KeyArgs& K, const ChaChaKey& ck, u64 nonce, size_t e) {
   constexpr int NB = (L1 + 15) / 16;
   const int topbits = K.nbits - 32 * (L1 - 1);
   const u32 topmask = topbits >= 32 ? 0xffffffffu : ((1u << topbits) - 1u);
-#pragma unroll
-  for (int j = L1; j < L; ++j) A[j] = 0;
   bool done = false;
   u32 attempt = 0;
   while (__any(!done)) {
@@ -192,7 +198,12 @@ __global__ __launch_bounds__(kBlock) void k_encrypt(KeyArgs K, const u32* __rest
 #pragma unroll
       for (int j = L1; j < L; ++j) A[j] = 0;
     } else {
-      draw_r<L>(A, K, ck, nonce, e);
+      u32 r[L1];
+      draw_r<L1>(r, K, ck, nonce, e);
+#pragma unroll
+      for (int j = 0; j < L1; ++j) A[j] = r[j];
+#pragma unroll
+      for (int j = L1; j < L; ++j) A[j] = 0;
     }
     slot_store_uniform<L>(slot, K.N2_R2);
     mont_mul<L>(A, slot, K.N2, K.n2_n0inv);                           // r R
@@ -201,6 +212,74 @@ __global__ __launch_bounds__(kBlock) void k_encrypt(KeyArgs K, const u32* __rest
     mont_mul<L>(A, slot, K.N2, K.n2_n0inv);                           // r^n * C_nude
     tile_store<L>(Ct, 0u, A);
     sout[e] = mneg ? 1 : 0;
+  }
+}
+
+// r for every element into a tile-major [ntiles][L1][64] buffer (ChaCha20 per element,
+// rejection sampling into [1, n-1]); kept out of the modexp kernel so its registers do
+// not count against the modexp's occupancy.
+template <int L1>
+__global__ __launch_bounds__(256) void k_draw_r(KeyArgs K, size_t count, ChaChaKey ck, u64 nonce, u32* __restrict__ R) {
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < count; e += (size_t)gridDim.x * blockDim.x) {
+    u32 r[L1];
+    draw_r<L1>(r, K, ck, nonce, e);
+#pragma unroll
+    for (int j = 0; j < L1; ++j) R[tiled(e, L1, j)] = r[j];
+  }
+}
+
+// Two lanes per element (mont2_dev.h) for 4096-bit n^2: lanes e / e+32 of a wave hold the
+// low / high 64 limbs of one element; a wave covers 32 elements (half a memory tile).
+template <int L, int W>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_encrypt2(KeyArgs K, const u32* __restrict__ P, u32 lp,
+                                                     const u8* __restrict__ neg, size_t count, int obf,
+                                                     const u32* __restrict__ rin, u32* __restrict__ Cout,
+                                                     u8* __restrict__ sout, u32* __restrict__ scratch) {
+  constexpr int LL = L / 2;  // limbs per lane (== limbs of n)
+  extern __shared__ __attribute__((aligned(16))) u32 lds[];
+  const WaveCtx w = wave_ctx();
+  const int e = w.lane & 31, h = w.lane >> 5;
+  const u32 wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  u32* bcol = lds + wib * (L * kHalf) + e;
+  const u32 hoff = half_off<LL>(h);
+  const Tile tb = make_tile(scratch + (size_t)w.gw * ((size_t)(1 << W) * LL * FPHE_WAVE), (1u << W) * LL * 256u, w.lane);
+  u32 NV[LL];
+#pragma unroll
+  for (int j = 0; j < LL; ++j) NV[j] = K.N2[h * LL + j];
+  const u32 nwt = (u32)((count + kHalf - 1) / kHalf);
+  for (u32 wt = w.gw; wt < nwt; wt += w.nw) {
+    const u32 tile = wt >> 1;
+    const u32 col = (wt & 1u) * kHalf + (u32)e;
+    const size_t elem = (size_t)tile * FPHE_WAVE + col;
+    Tile Pt = make_tile(P + (size_t)tile * lp * FPHE_WAVE, lp * 256u, 0);
+    Pt.vo = col * 4u;
+    Tile Ct = make_tile(Cout + (size_t)tile * L * FPHE_WAVE, L * 256u, 0);
+    Ct.vo = ((u32)h * LL * FPHE_WAVE + col) * 4u;
+    bool mneg = false;
+    if (h == 0) mneg = nude_to_slot<L, kHalf>(bcol, K, Pt, lp, neg[elem] != 0);
+    if (!obf) {
+#pragma unroll
+      for (int j = 0; j < LL; ++j) Ct.st(bcol[hoff + j * kHalf], j * 256u);
+      if (h == 0) sout[elem] = mneg ? 1 : 0;
+      continue;
+    }
+    slot2_to_tile<LL>(tb, 0u, bcol, hoff);  // stash this lane's half of C_nude in table entry 0
+    // r: injected, or drawn beforehand into the same buffer by k_draw_r (launch_encrypt)
+    u32 A[LL];
+    {
+      Tile Rt = make_tile(rin + (size_t)tile * LL * FPHE_WAVE, LL * 256u, 0);
+      Rt.vo = col * 4u;
+#pragma unroll
+      for (int j = 0; j < LL; ++j) A[j] = h == 0 ? Rt.ld(j * 256u) : 0u;
+    }
+    slot2_store_uniform<LL>(bcol, K.N2_R2, hoff, h);
+    mont_mul2<LL>(A, bcol, NV, K.n2_n0inv);                                   // r R
+    powm_uniform2<LL, W>(A, bcol, tb, NV, K.n2_n0inv, K.n, K.nbits, hoff);  // r^n R
+    tile2_to_slot<LL>(bcol, tb, 0u, hoff);
+    mont_mul2<LL>(A, bcol, NV, K.n2_n0inv);                                   // r^n * C_nude
+#pragma unroll
+    for (int j = 0; j < LL; ++j) Ct.st(A[j], j * 256u);
+    if (h == 0) sout[elem] = mneg ? 1 : 0;
   }
 }
 
@@ -520,10 +599,6 @@ __global__ __launch_bounds__(kBlock) void k_mul(KeyArgs K, const u32* __restrict
 // ======================================================================================
 // fixed-point encode / decode (fixedpoint_paillier/src/lib.rs:148-192)
 // ======================================================================================
-__device__ __forceinline__ size_t tiled(size_t e, u32 lp, u32 j) {
-  return ((e >> 6) * lp + j) * FPHE_WAVE + (e & 63);
-}
-
 __device__ __forceinline__ u32 encode_core(double x, u64& mag, bool& ng, int& ex) {
   const u64 b = (u64)__double_as_longlong(x);
   const int E = (int)((b >> 52) & 0x7ff);
@@ -734,6 +809,32 @@ template <int L>
 fphe_status launch_encrypt(fphe_ctx* c, const uint32_t* P, uint32_t lp, const uint8_t* neg, size_t count,
                                   int obf, const uint32_t* r, const uint32_t key[8], uint64_t nonce, uint32_t* C,
                                   uint8_t* sign, hipStream_t s) {
+  if constexpr (L == 128) {  // two lanes per element: 2 waves/SIMD (VGPR), 2 workgroups/CU (64 KiB LDS each)
+    constexpr int LL = L / 2;
+    const size_t waves = (count + kHalf - 1) / kHalf;
+    size_t g = (size_t)c->cus * 2;
+    const size_t need = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
+    if (need < g) g = need;
+    const unsigned grid = (unsigned)(g ? g : 1);
+    const size_t lds = (size_t)kWavesPerBlock * L * kHalf * 4;
+    const size_t tbytes = (size_t)grid * kWavesPerBlock * (1u << kWinEnc) * LL * FPHE_WAVE * 4;
+    const size_t rbytes = (size_t)ntiles_of(count) * LL * FPHE_WAVE * 4;
+    if (ensure_scratch(c, tbytes + (r ? 0 : rbytes)) != FPHE_OK) return FPHE_ERR_HIP;
+    const u32* rbuf = r;
+    if (obf && !r) {
+      u32* rdev = c->scratch + tbytes / 4;
+      ChaChaKey ck;
+      for (int i = 0; i < 8; ++i) ck.k[i] = key[i];
+      const unsigned rgrid = (unsigned)std::min<size_t>((count + 255) / 256, (size_t)c->cus * 4);
+      hipLaunchKernelGGL(k_draw_r<LL>, dim3(rgrid), dim3(256), 0, s, c->K, count, ck, nonce, rdev);
+      rbuf = rdev;
+    }
+    auto kern = k_encrypt2<L, kWinEnc>;
+    set_lds(kern, lds);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, P, lp, neg, count, obf, rbuf, C, sign,
+                       c->scratch);
+    return hip_ok(hipGetLastError());
+  }
   const int bpc = bpc_for_slot(L);
   const unsigned grid = grid_for(c, count, bpc);
   const size_t lds = (size_t)kWavesPerBlock * L * FPHE_WAVE * 4;
