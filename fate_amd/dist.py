@@ -1,0 +1,88 @@
+"""Element sharding of the PHE hot path across the GPUs of a node (one process per GPU).
+
+Paillier encrypt / decrypt / ct-add / ct x pt are independent per element, so a tensor of
+``count`` elements is split into contiguous, tile-aligned (64-element) ranges, one per rank
+-- the same decomposition as the reference's ``DTensor.map_shard``
+(python/fate/arch/tensor/distributed/_tensor.py:365-385), with GPUs instead of computing
+partitions.  The only exchange step is the optional all-gather of the ciphertext shards
+when the consumer needs the whole vector in one place (e.g. the federation sender on rank
+0): one ``all_gather_into_tensor`` of the byte-packed tiles per component, over RCCL/xGMI
+on GPUs (backend "nccl") or gloo on CPU.  Reductions across ranks would be gather-then-
+modmul (RCCL has no modular-product reduce); ciphertext reductions are order independent
+(SURVEY.md §0 fact 3), so that stays bit-exact.
+"""
+from __future__ import annotations
+
+from typing import Tuple
+
+import torch
+
+WAVE = 64
+
+
+def shard_bounds(count: int, rank: int, world: int) -> Tuple[int, int]:
+    """[start, end) of rank's elements: contiguous, 64-aligned (whole tiles), balanced."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError("bad rank/world")
+    tiles = (count + WAVE - 1) // WAVE
+    base, extra = divmod(tiles, world)
+    t0 = rank * base + min(rank, extra)
+    t1 = t0 + base + (1 if rank < extra else 0)
+    return min(t0 * WAVE, count), min(t1 * WAVE, count)
+
+
+def gather_tiles(C: torch.Tensor, sign: torch.Tensor, exp: torch.Tensor, count: int, group=None):
+    """All-gather the per-rank shards (tile-major C [nt, L, 64], sign/exp [nt*64]) into the
+    full vector on every rank.  Shards are padded to the largest shard for the collective
+    and trimmed after.  Returns (C, sign, exp, total_count)."""
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    dev = C.device
+    cnt = torch.tensor([count], dtype=torch.int64, device=dev)
+    counts = [torch.zeros_like(cnt) for _ in range(world)]
+    dist.all_gather(counts, cnt, group=group)
+    counts = [int(c.item()) for c in counts]
+    nt_max = max((c + WAVE - 1) // WAVE for c in counts) if counts else 0
+    L = C.shape[1]
+
+    def pad_tiles(t: torch.Tensor) -> torch.Tensor:
+        if t.shape[0] == nt_max:
+            return t.contiguous()
+        out = t.new_zeros((nt_max,) + tuple(t.shape[1:]))
+        out[: t.shape[0]] = t
+        return out
+
+    def pad_flat(t: torch.Tensor) -> torch.Tensor:
+        n = nt_max * WAVE
+        if t.shape[0] == n:
+            return t.contiguous()
+        out = t.new_zeros(n)
+        out[: t.shape[0]] = t
+        return out
+
+    Cg = torch.empty((world * nt_max, L, WAVE), dtype=C.dtype, device=dev)
+    dist.all_gather_into_tensor(Cg, pad_tiles(C), group=group)
+    # sign is uint8: gather as int32 for backend portability (gloo lacks uint8 on some builds)
+    sg = torch.empty(world * nt_max * WAVE, dtype=torch.int32, device=dev)
+    dist.all_gather_into_tensor(sg, pad_flat(sign.to(torch.int32)), group=group)
+    eg = torch.empty(world * nt_max * WAVE, dtype=exp.dtype, device=dev)
+    dist.all_gather_into_tensor(eg, pad_flat(exp), group=group)
+    # shards are whole tiles except possibly the last rank's: drop the per-rank padding
+    Cs, ss, es = [], [], []
+    for r, c in enumerate(counts):
+        nt = (c + WAVE - 1) // WAVE
+        Cs.append(Cg[r * nt_max: r * nt_max + nt])
+        ss.append(sg[r * nt_max * WAVE: r * nt_max * WAVE + nt * WAVE])
+        es.append(eg[r * nt_max * WAVE: r * nt_max * WAVE + nt * WAVE])
+    total = sum(counts)
+    return torch.cat(Cs), torch.cat(ss).to(torch.uint8), torch.cat(es), total
+
+
+def gather_ciphertexts(cv, group=None):
+    """All-gather a sharded ``fate_amd.paillier.CiphertextVector`` (every shard but the last
+    must be whole tiles, as produced by :func:`shard_bounds`)."""
+    from .paillier import CiphertextVector
+
+    C, s, e, n = gather_tiles(cv.C, cv.sign, cv.exp, cv.count, group)
+    return CiphertextVector(C, s, e, n)

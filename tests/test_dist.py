@@ -1,0 +1,76 @@
+"""Multi-process (world_size 2, gloo, CPU) tests of the element sharding and the ciphertext
+all-gather used for N>1 GPUs (fate_amd/dist.py).  The data-path collective is exercised on
+CPU tensors in the same tile-major layout the GPU kernels produce."""
+import os
+import socket
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from fate_amd.dist import WAVE, gather_tiles, shard_bounds
+
+
+def test_shard_bounds_cover_and_align():
+    for count in [0, 1, 63, 64, 65, 1000, 1 << 20, 100_000_001]:
+        for world in [1, 2, 3, 4, 8]:
+            spans = [shard_bounds(count, r, world) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == count
+            for (a0, a1), (b0, b1) in zip(spans, spans[1:]):
+                assert a1 == b0
+            for (s, e), (s2, e2) in zip(spans, spans[1:]):
+                if e2 > s2:  # every shard followed by a non-empty one is whole tiles
+                    assert s % WAVE == 0 and (e - s) % WAVE == 0
+            sizes = [e - s for s, e in spans]
+            assert max(sizes) - min(sizes) < 2 * WAVE  # one tile of imbalance + a partial last tile
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, count, L, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # full vector: element e, limb j = e * 1000 + j (tile-major)
+        full = torch.arange(count, dtype=torch.int64)
+        s, e = shard_bounds(count, rank, world)
+        n = e - s
+        nt = (n + WAVE - 1) // WAVE
+        C = torch.zeros((nt, L, WAVE), dtype=torch.int32)
+        sign = torch.zeros(nt * WAVE, dtype=torch.uint8)
+        exp = torch.zeros(nt * WAVE, dtype=torch.int32)
+        for k in range(n):
+            g = s + k
+            C[k // WAVE, :, k % WAVE] = torch.tensor([g * 1000 + j for j in range(L)], dtype=torch.int32)
+            sign[k] = g % 2
+            exp[k] = -(g % 7)
+        Cg, sg, eg, total = gather_tiles(C, sign, exp, n)
+        ok = total == count
+        for g in range(count):
+            ok &= bool(torch.equal(Cg[g // WAVE, :, g % WAVE],
+                                   torch.tensor([g * 1000 + j for j in range(L)], dtype=torch.int32)))
+            ok &= int(sg[g]) == g % 2 and int(eg[g]) == -(g % 7)
+        q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_tiles_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    count, L, world = 200, 5, 2  # rank 0: 128 (2 tiles), rank 1: 72 (partial last tile)
+    procs = [ctx.Process(target=_worker, args=(r, world, port, count, L, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: True, 1: True}
