@@ -46,6 +46,18 @@ def enc_mac32_per_elem(key_bits: int) -> float:
     return (E + math.ceil(E / 5) + 16 + 1) * mac32_per_mont(L)
 
 
+def enc_products_per_elem(key_bits: int) -> int:
+    E = key_bits
+    return E + math.ceil(E / 5) + 16 + 1
+
+
+def enc_mad27_per_elem(key_bits: int) -> float:
+    # issued v_mad_u64_u32 of the reduced-radix engine (fate_amd/csrc/mont27_dev.h): a
+    # product over NL 27-bit limbs is NL rows x 2 NL MACs; NL = 152 for 4096-bit n^2.
+    NL = 38 * (key_bits // 16 // 32)
+    return enc_products_per_elem(key_bits) * 2 * NL * NL
+
+
 def dec_mac32_per_elem(key_bits: int) -> float:
     E = key_bits // 2
     L = key_bits // 32
@@ -195,9 +207,11 @@ def main() -> None:
     achieved = mac_launch / (enc_kernel_ms / 1e3) / 1e12
     # algorithmic HBM bytes per element: f32 sig/exp/neg read (13 B) + C (512 B) + sign (1 B) written
     hbm_bytes = N * (8 + 1 + 4 + key_bits // 4 + 1)
+    r27 = os.environ.get("FPHE_ENGINE", "27") != "32"
+    mad27 = N * enc_mad27_per_elem(key_bits) / (enc_kernel_ms / 1e3) / 1e12
     roofline = {
         "bound": "valu",
-        "kernel": "k_encrypt<128,5>",
+        "kernel": "k_encrypt27<128,5> (+k_draw_r)" if r27 else "k_encrypt2<128,5> (+k_draw_r)",
         "achieved": round(achieved, 3),
         "peak": round(PEAK_TMAC32, 3),
         "unit": "TMAC32/s",
@@ -205,6 +219,10 @@ def main() -> None:
         "traffic": None,
         "per_elem_mac32": enc_mac32_per_elem(key_bits),
         "kernel_ms": round(enc_kernel_ms, 3),
+        # instruction-issue view of the same launch: 27-bit-limb MACs issued (one
+        # v_mad_u64_u32 each) against the same half-rate mad peak
+        "issue": {"mad64_per_elem": enc_mad27_per_elem(key_bits), "achieved": round(mad27, 3),
+                  "peak": round(PEAK_TMAC32, 3), "unit": "Tmad/s", "frac": round(mad27 / PEAK_TMAC32, 4)} if r27 else None,
         "hbm": {"achieved": round(hbm_bytes / (enc_kernel_ms / 1e3) / 1e9, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s"},
     }
     out = {

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
+#include <stdlib.h>
 #include <vector>
 #include <mutex>
 
@@ -42,6 +43,11 @@ struct KeyArgs {
   const u32* pinvqR;   // p^{-1} mod q, times R_q mod q
   u32 p2_n0inv, p_n0inv, q2_n0inv, q_n0inv;
   int pm1_bits, qm1_bits;
+  // reduced-radix engine (kernels27.h): 27-bit limbs, R = 2^(27 NL)
+  const u32* N2_27; const u32* N2R1_27; const u32* N2R2_27;  // n^2, R mod n^2, R^2 mod n^2 [NL2]
+  const u32* P2_27; const u32* P2R1_27; const u32* P2R2_27;  // p^2 ...                      [NLh]
+  const u32* Q2_27; const u32* Q2R1_27; const u32* Q2R2_27;
+  u32 n2_np27, p2_np27, q2_np27;                             // -N^{-1} mod 2^27
 };
 
 __device__ __forceinline__ void set_err(int32_t* err, u32 f) {
@@ -286,13 +292,55 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 // ======================================================================================
 // decrypt (CRT): crates/paillier/src/lib.rs:163-176
 // ======================================================================================
+// d_s = L_s(y) * h_s mod s from y = c^(s-1) mod s^2 (LH words): paillier/src/lib.rs:174-176
+template <int L>
+__device__ __forceinline__ void crt_tail(u32 (&dout)[L / 4], const u32 (&A)[L / 2], u32* slot,
+                                         const u32* __restrict__ S, u32 s_n0inv, const u32* __restrict__ sinv2,
+                                         const u32* __restrict__ hsR) {
+  constexpr int LH = L / 2, LQ = L / 4;
+  // L(y) = (y - 1) / s, exact for units: (y-1) * s^{-1} mod 2^(32 LQ)
+  u32 nz = 0;
+#pragma unroll
+  for (int j = 0; j < LH; ++j) nz |= A[j];
+  u32 y1[LQ];
+  {
+    u32 br = 1;
+#pragma unroll
+    for (int j = 0; j < LQ; ++j) {
+      const u64 d = (u64)A[j] - br;
+      y1[j] = (u32)d;
+      br = (u32)(d >> 63);
+    }
+  }
+  u32 Ls[LQ];
+#pragma unroll
+  for (int j = 0; j < LQ; ++j) Ls[j] = 0;
+#pragma unroll
+  for (int i = 0; i < LQ; ++i) {
+    u64 acc = 0;
+#pragma unroll
+    for (int j = 0; i + j < LQ; ++j) {
+      acc = (u64)y1[i] * sinv2[j] + Ls[i + j] + (acc >> 32);
+      Ls[i + j] = (u32)acc;
+    }
+  }
+  if (nz == 0) {  // y == 0: reference computes (0-1)/s = 0 (truncating)
+#pragma unroll
+    for (int j = 0; j < LQ; ++j) Ls[j] = 0;
+  }
+  slot_store_uniform<LQ>(slot, hsR);
+  mont_mul<LQ>(Ls, slot, S, s_n0inv);  // L * h_s mod s
+#pragma unroll
+  for (int j = 0; j < LQ; ++j) dout[j] = Ls[j];
+}
+
 // d_s = L_s(c^(s-1) mod s^2) * h_s mod s  for s in {p, q}
 template <int L, int W>
 __device__ __forceinline__ void crt_half(u32 (&dout)[L / 4], const Tile& Cin, u32* slot, const Tile& tb,
                                          const u32* __restrict__ S2, u32 s2_n0inv, const u32* __restrict__ S2_R3,
                                          const u32* __restrict__ sm1, int sm1_bits, const u32* __restrict__ S,
                                          u32 s_n0inv, const u32* __restrict__ sinv2, const u32* __restrict__ hsR) {
-  constexpr int LH = L / 2, LQ = L / 4;
+  constexpr int LH = L / 2;
   u32 A[LH];
   {
     // REDC of the 2LH-limb c modulo S2 (c < n^2 < S2 * 2^(32 LH))
@@ -332,40 +380,57 @@ __device__ __forceinline__ void crt_half(u32 (&dout)[L / 4], const Tile& Cin, u3
   powm_uniform<LH, W>(A, slot, tb, S2, s2_n0inv, sm1, sm1_bits);  // c^(s-1) R
   slot_store_small<LH>(slot, 1u);
   mont_mul<LH>(A, slot, S2, s2_n0inv);                            // y = c^(s-1) mod s^2
-  // L(y) = (y - 1) / s, exact for units: (y-1) * s^{-1} mod 2^(32 LQ)
-  u32 nz = 0;
+  crt_tail<L>(dout, A, slot, S, s_n0inv, sinv2, hsR);
+}
+
+// m = dp + p * ((dq - dp) p^{-1} mod q): paillier/src/lib.rs:163-172
+template <int L>
+__device__ __forceinline__ void crt_combine(const u32 (&dp)[L / 4], const u32 (&dq)[L / 4], const KeyArgs& K,
+                                            u32* slot, const Tile& Pt) {
+  constexpr int LQ = L / 4;
+  // u = (dq - dp) mod q ; u = u * p^{-1} mod q  (paillier/src/lib.rs:166, canonical form; the
+  // reference's `if o < 0 { o += n }` at :168-170 lands on the same value)
+  u32 u[LQ];
+  u32 br = 0;
 #pragma unroll
-  for (int j = 0; j < LH; ++j) nz |= A[j];
-  u32 y1[LQ];
-  {
-    u32 br = 1;
+  for (int j = 0; j < LQ; ++j) {
+    const u64 d = (u64)dq[j] - dp[j] - br;
+    u[j] = (u32)d;
+    br = (u32)(d >> 63);
+  }
+  if (br) {
+    u32 c = 0;
 #pragma unroll
     for (int j = 0; j < LQ; ++j) {
-      const u64 d = (u64)A[j] - br;
-      y1[j] = (u32)d;
-      br = (u32)(d >> 63);
+      const u64 t = (u64)u[j] + K.q[j] + c;
+      u[j] = (u32)t;
+      c = (u32)(t >> 32);
     }
   }
-  u32 Ls[LQ];
+  slot_store_uniform<LQ>(slot, K.pinvqR);
+  mont_mul<LQ>(u, slot, K.q, K.q_n0inv);
+  // m = u * p + dp  (p uniform outer operand, shifting accumulator; limb i final after step i)
+  u32 T[LQ + 1];
 #pragma unroll
-  for (int j = 0; j < LQ; ++j) Ls[j] = 0;
-#pragma unroll
+  for (int j = 0; j < LQ; ++j) T[j] = dp[j];
+  T[LQ] = 0;
+#pragma unroll 1
   for (int i = 0; i < LQ; ++i) {
+    const u32 pi = K.p[i];
     u64 acc = 0;
 #pragma unroll
-    for (int j = 0; i + j < LQ; ++j) {
-      acc = (u64)y1[i] * sinv2[j] + Ls[i + j] + (acc >> 32);
-      Ls[i + j] = (u32)acc;
+    for (int j = 0; j < LQ; ++j) {
+      acc = (u64)u[j] * pi + T[j] + (acc >> 32);
+      T[j] = (u32)acc;
     }
-  }
-  if (nz == 0) {  // y == 0: reference computes (0-1)/s = 0 (truncating)
+    T[LQ] += (u32)(acc >> 32);
+    Pt.st(T[0], (u32)i * 256u);
 #pragma unroll
-    for (int j = 0; j < LQ; ++j) Ls[j] = 0;
+    for (int j = 0; j < LQ; ++j) T[j] = T[j + 1];
+    T[LQ] = 0;
   }
-  slot_store_uniform<LQ>(slot, hsR);
-  mont_mul<LQ>(Ls, slot, S, s_n0inv);  // L * h_s mod s
 #pragma unroll
-  for (int j = 0; j < LQ; ++j) dout[j] = Ls[j];
+  for (int j = 0; j < LQ; ++j) Pt.st(T[j], (u32)(LQ + j) * 256u);
 }
 
 template <int L, int W>
@@ -382,49 +447,33 @@ __global__ __launch_bounds__(kBlock) void k_decrypt(KeyArgs K, const u32* __rest
     u32 dp[LQ], dq[LQ];
     crt_half<L, W>(dp, Cin, slot, tb, K.P2, K.p2_n0inv, K.P2_R3, K.pm1, K.pm1_bits, K.p, K.p_n0inv, K.pinv2, K.hpR);
     crt_half<L, W>(dq, Cin, slot, tb, K.Q2, K.q2_n0inv, K.Q2_R3, K.qm1, K.qm1_bits, K.q, K.q_n0inv, K.qinv2, K.hqR);
-    // u = (dq - dp) mod q ; u = u * p^{-1} mod q  (paillier/src/lib.rs:166, canonical form; the
-    // reference's `if o < 0 { o += n }` at :168-170 lands on the same value)
-    u32 u[LQ];
-    u32 br = 0;
-#pragma unroll
-    for (int j = 0; j < LQ; ++j) {
-      const u64 d = (u64)dq[j] - dp[j] - br;
-      u[j] = (u32)d;
-      br = (u32)(d >> 63);
+    crt_combine<L>(dp, dq, K, slot, Pt);
+  }
+}
+
+// decrypt, CRT phase for the reduced-radix path: y_p, y_q (k_decrypt_pow27) -> m.
+template <int L>
+__global__ __launch_bounds__(kBlock) void k_decrypt_crt(KeyArgs K, const u32* __restrict__ Y, u32 ntiles,
+                                                        u32* __restrict__ Pout) {
+  constexpr int LH = L / 2, LQ = L / 4;
+  extern __shared__ __attribute__((aligned(16))) u32 lds[];
+  const WaveCtx w = wave_ctx();
+  u32* slot = lds_slot<LQ>(lds, w.lane);
+  for (u32 tile = w.gw; tile < ntiles; tile += w.nw) {
+    const Tile Yt = make_tile(Y + (size_t)tile * 2 * LH * FPHE_WAVE, 2 * LH * 256u, w.lane);
+    const Tile Pt = make_tile(Pout + (size_t)tile * LH * FPHE_WAVE, LH * 256u, w.lane);
+    u32 dp[LQ], dq[LQ];
+    {
+      u32 A[LH];
+      tile_load<LH>(A, Yt, 0u);
+      crt_tail<L>(dp, A, slot, K.p, K.p_n0inv, K.pinv2, K.hpR);
     }
-    if (br) {
-      u32 c = 0;
-#pragma unroll
-      for (int j = 0; j < LQ; ++j) {
-        const u64 t = (u64)u[j] + K.q[j] + c;
-        u[j] = (u32)t;
-        c = (u32)(t >> 32);
-      }
+    {
+      u32 A[LH];
+      tile_load<LH>(A, Yt, LH * 256u);
+      crt_tail<L>(dq, A, slot, K.q, K.q_n0inv, K.qinv2, K.hqR);
     }
-    slot_store_uniform<LQ>(slot, K.pinvqR);
-    mont_mul<LQ>(u, slot, K.q, K.q_n0inv);
-    // m = u * p + dp  (p uniform outer operand, shifting accumulator; limb i final after step i)
-    u32 T[LQ + 1];
-#pragma unroll
-    for (int j = 0; j < LQ; ++j) T[j] = dp[j];
-    T[LQ] = 0;
-#pragma unroll 1
-    for (int i = 0; i < LQ; ++i) {
-      const u32 pi = K.p[i];
-      u64 acc = 0;
-#pragma unroll
-      for (int j = 0; j < LQ; ++j) {
-        acc = (u64)u[j] * pi + T[j] + (acc >> 32);
-        T[j] = (u32)acc;
-      }
-      T[LQ] += (u32)(acc >> 32);
-      Pt.st(T[0], (u32)i * 256u);
-#pragma unroll
-      for (int j = 0; j < LQ; ++j) T[j] = T[j + 1];
-      T[LQ] = 0;
-    }
-#pragma unroll
-    for (int j = 0; j < LQ; ++j) Pt.st(T[j], (u32)(LQ + j) * 256u);
+    crt_combine<L>(dp, dq, K, slot, Pt);
   }
 }
 
@@ -742,6 +791,8 @@ __global__ __launch_bounds__(256) void k_decode_f64(KeyArgs K, const u32* __rest
 
 }  // namespace
 
+#include "kernels27.h"
+
 // ======================================================================================
 // host side: context + C ABI
 // ======================================================================================
@@ -755,6 +806,7 @@ struct fphe_ctx {
   KeyArgs K{};
   u32* scratch = nullptr;
   size_t scratch_bytes = 0;
+  bool r27 = true;  // reduced-radix engine (FPHE_ENGINE=32 selects the 32-bit-limb kernels)
   std::mutex mu;
 };
 
@@ -771,6 +823,29 @@ struct DevGuard {
 };
 
 Limbs from_words(const uint32_t* w, size_t n) { return hbn::norm(Limbs(w, w + n)); }
+
+// little-endian 32-bit words -> nl 27-bit limbs
+Limbs to27(const Limbs& v, int nl) {
+  Limbs o((size_t)nl, 0u);
+  for (int i = 0; i < nl; ++i) {
+    const size_t bit = (size_t)27 * i, w = bit >> 5;
+    const unsigned off = (unsigned)(bit & 31);
+    u64 x = w < v.size() ? v[w] : 0u;
+    if (w + 1 < v.size()) x |= (u64)v[w + 1] << 32;
+    o[(size_t)i] = (u32)(x >> off) & ((1u << 27) - 1u);
+  }
+  return o;
+}
+
+template <typename KernT>
+unsigned occ_grid(const fphe_ctx* c, KernT k, size_t lds, size_t waves) {
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kBlock, lds) != hipSuccess || nb < 1) nb = 1;
+  size_t g = (size_t)c->cus * (size_t)nb;
+  const size_t need = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
+  if (need < g) g = need;
+  return (unsigned)(g ? g : 1);
+}
 
 // Grid: `bpc` workgroups per CU (from LDS/VGPR budget), capped by the work.
 u32 ntiles_of(size_t count) { return (u32)((count + FPHE_WAVE - 1) / FPHE_WAVE); }
@@ -893,6 +968,85 @@ fphe_status launch_mul(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, const
   return hip_ok(hipGetLastError());
 }
 
+
+// ---- reduced-radix engine launchers (kernels27.h) ---------------------------------------
+template <int L>
+fphe_status launch_encrypt27(fphe_ctx* c, const uint32_t* P, uint32_t lp, const uint8_t* neg, size_t count, int obf,
+                             const uint32_t* r, const uint32_t key[8], uint64_t nonce, uint32_t* C, uint8_t* sign,
+                             hipStream_t s) {
+  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = r27::LL * TPI, LDSW = NL > L ? NL : L, L1 = L / 2;
+  auto kern = k_encrypt27<L, kWinEnc>;
+  const size_t lds = (size_t)kWavesPerBlock * LDSW * E * 4;
+  set_lds(kern, lds);
+  const unsigned grid = occ_grid(c, kern, lds, (count + E - 1) / E);
+  const size_t tbytes = (size_t)grid * kWavesPerBlock * (1u << kWinEnc) * r27::LL * FPHE_WAVE * 4;
+  const size_t rbytes = (size_t)ntiles_of(count) * L1 * FPHE_WAVE * 4;
+  const bool draw = obf && !r;
+  if (ensure_scratch(c, tbytes + (draw ? rbytes : 0)) != FPHE_OK) return FPHE_ERR_HIP;
+  const u32* rbuf = r;
+  if (draw) {
+    u32* rdev = c->scratch + tbytes / 4;
+    ChaChaKey ck;
+    for (int i = 0; i < 8; ++i) ck.k[i] = key[i];
+    const unsigned rgrid = (unsigned)std::min<size_t>((count + 255) / 256, (size_t)c->cus * 4);
+    hipLaunchKernelGGL(k_draw_r<L1>, dim3(rgrid), dim3(256), 0, s, c->K, count, ck, nonce, rdev);
+    rbuf = rdev;
+  }
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, P, lp, neg, count, obf, rbuf, C, sign, c->scratch,
+                     (u32)LDSW);
+  return hip_ok(hipGetLastError());
+}
+
+template <int L>
+fphe_status launch_decrypt27(fphe_ctx* c, const uint32_t* C, size_t count, uint32_t* P, hipStream_t s) {
+  constexpr int TPI = L / 64, E = FPHE_WAVE / TPI, NL = r27::LL * TPI, LH = L / 2, LQ = L / 4;
+  auto kern = k_decrypt_pow27<L, kWinEnc>;
+  const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
+  set_lds(kern, lds);
+  const unsigned grid = occ_grid(c, kern, lds, (count + E - 1) / E);
+  const size_t tbytes = (size_t)grid * kWavesPerBlock * (1u << kWinEnc) * r27::LL * FPHE_WAVE * 4;
+  const size_t ybytes = (size_t)ntiles_of(count) * 2 * LH * FPHE_WAVE * 4;
+  if (ensure_scratch(c, tbytes + ybytes) != FPHE_OK) return FPHE_ERR_HIP;
+  u32* Y = c->scratch + tbytes / 4;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, C, count, Y, c->scratch, (u32)NL);
+  auto kcrt = k_decrypt_crt<L>;
+  const size_t lds2 = (size_t)kWavesPerBlock * LQ * FPHE_WAVE * 4;
+  set_lds(kcrt, lds2);
+  const unsigned grid2 = grid_for(c, count, bpc_for_slot(LQ));
+  hipLaunchKernelGGL(kcrt, dim3(grid2), dim3(kBlock), lds2, s, c->K, Y, ntiles_of(count), P);
+  return hip_ok(hipGetLastError());
+}
+
+template <int L>
+fphe_status launch_add27(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, const int32_t* ea, const uint32_t* Cb,
+                         const uint8_t* sb, const int32_t* eb, int bstride, size_t count, uint32_t* Co, uint8_t* so,
+                         int32_t* eo, hipStream_t s) {
+  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = r27::LL * TPI;
+  auto kern = k_add27<L>;
+  const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
+  set_lds(kern, lds);
+  const unsigned grid = occ_grid(c, kern, lds, (count + E - 1) / E);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, Ca, sa, ea, Cb, sb, eb, bstride, count, Co, so, eo,
+                     (u32)NL);
+  return hip_ok(hipGetLastError());
+}
+
+template <int L>
+fphe_status launch_mul27(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, const int32_t* ea, const uint32_t* P,
+                         uint32_t lp, const uint8_t* pneg, const int32_t* pexp, int pstride, size_t count,
+                         uint32_t* Co, uint8_t* so, int32_t* eo, int32_t* err, hipStream_t s) {
+  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = r27::LL * TPI;
+  auto kern = k_mul27<L, kWinMul>;
+  const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
+  set_lds(kern, lds);
+  const unsigned grid = occ_grid(c, kern, lds, (count + E - 1) / E);
+  const size_t tbytes = (size_t)grid * kWavesPerBlock * (1u << kWinMul) * r27::LL * FPHE_WAVE * 4;
+  if (ensure_scratch(c, tbytes) != FPHE_OK) return FPHE_ERR_HIP;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, Ca, sa, ea, P, lp, pneg, pexp, pstride, count, Co,
+                     so, eo, err, c->scratch, (u32)NL);
+  return hip_ok(hipGetLastError());
+}
+
 }  // namespace
 
 extern "C" {
@@ -928,6 +1082,11 @@ fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, 
     max_int = hbn::norm(max_int);
     const size_t o_max = put(max_int, L1);
     const size_t o_nmm = put(hbn::sub(n, max_int), L1);
+    const int NL2 = 38 * (L2 / 32), NLh = 38 * (L2 / 64);
+    const size_t o_N2_27 = put(to27(N2, NL2), NL2);
+    const size_t o_N2R1_27 = put(to27(hbn::pow2_mod((size_t)27 * NL2, N2), NL2), NL2);
+    const size_t o_N2R2_27 = put(to27(hbn::pow2_mod((size_t)54 * NL2, N2), NL2), NL2);
+    size_t o_P2_27 = 0, o_P2R1_27 = 0, o_P2R2_27 = 0, o_Q2_27 = 0, o_Q2R1_27 = 0, o_Q2R2_27 = 0;
     size_t o_P2 = 0, o_P2R3 = 0, o_pm1 = 0, o_p = 0, o_pinv2 = 0, o_hpR = 0;
     size_t o_Q2 = 0, o_Q2R3 = 0, o_qm1 = 0, o_q = 0, o_qinv2 = 0, o_hqR = 0, o_pinvqR = 0;
     u32 p2n0 = 0, pn0 = 0, q2n0 = 0, qn0 = 0;
@@ -962,6 +1121,12 @@ fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, 
       o_qinv2 = put(hbn::inv_pow2(q, LQ), LQ);
       o_hqR = put(hbn::mod(hbn::mul(hq, hbn::pow2_mod((size_t)32 * LQ, q)), q), LQ);
       o_pinvqR = put(hbn::mod(hbn::mul(pinvq, hbn::pow2_mod((size_t)32 * LQ, q)), q), LQ);
+      o_P2_27 = put(to27(P2, NLh), NLh);
+      o_P2R1_27 = put(to27(hbn::pow2_mod((size_t)27 * NLh, P2), NLh), NLh);
+      o_P2R2_27 = put(to27(hbn::pow2_mod((size_t)54 * NLh, P2), NLh), NLh);
+      o_Q2_27 = put(to27(Q2, NLh), NLh);
+      o_Q2R1_27 = put(to27(hbn::pow2_mod((size_t)27 * NLh, Q2), NLh), NLh);
+      o_Q2R2_27 = put(to27(hbn::pow2_mod((size_t)54 * NLh, Q2), NLh), NLh);
       p2n0 = hbn::neg_inv32(P2[0]); pn0 = hbn::neg_inv32(p[0]);
       q2n0 = hbn::neg_inv32(Q2[0]); qn0 = hbn::neg_inv32(q[0]);
       pm1b = (int)hbn::bitlen(pm1); qm1b = (int)hbn::bitlen(qm1);
@@ -982,12 +1147,21 @@ fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, 
     K.max_int = b + o_max; K.n_mm = b + o_nmm;
     K.n2_n0inv = hbn::neg_inv32(N2[0]);
     K.nbits = (int)key_bits;
+    K.N2_27 = b + o_N2_27; K.N2R1_27 = b + o_N2R1_27; K.N2R2_27 = b + o_N2R2_27;
+    K.n2_np27 = K.n2_n0inv & ((1u << 27) - 1u);
+    {
+      const char* eng = getenv("FPHE_ENGINE");
+      c->r27 = !(eng && strcmp(eng, "32") == 0);
+    }
     if (has_sk) {
       K.P2 = b + o_P2; K.P2_R3 = b + o_P2R3; K.pm1 = b + o_pm1; K.p = b + o_p; K.pinv2 = b + o_pinv2; K.hpR = b + o_hpR;
       K.Q2 = b + o_Q2; K.Q2_R3 = b + o_Q2R3; K.qm1 = b + o_qm1; K.q = b + o_q; K.qinv2 = b + o_qinv2; K.hqR = b + o_hqR;
       K.pinvqR = b + o_pinvqR;
       K.p2_n0inv = p2n0; K.p_n0inv = pn0; K.q2_n0inv = q2n0; K.q_n0inv = qn0;
       K.pm1_bits = pm1b; K.qm1_bits = qm1b;
+      K.P2_27 = b + o_P2_27; K.P2R1_27 = b + o_P2R1_27; K.P2R2_27 = b + o_P2R2_27;
+      K.Q2_27 = b + o_Q2_27; K.Q2R1_27 = b + o_Q2R1_27; K.Q2R2_27 = b + o_Q2R2_27;
+      K.p2_np27 = p2n0 & ((1u << 27) - 1u); K.q2_np27 = q2n0 & ((1u << 27) - 1u);
     }
     *out = c;
     return FPHE_OK;
@@ -1075,6 +1249,11 @@ fphe_status fphe_encrypt(fphe_ctx* c, const uint32_t* P, uint32_t lp, const uint
   if (obf && !r && !rng_key) return FPHE_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DevGuard g(c->device);
+  if (c->r27) {
+    if (c->L2 == 128)
+      return launch_encrypt27<128>(c, P, lp, neg, count, obf, r, rng_key, nonce, C, sign, (hipStream_t)stream);
+    return launch_encrypt27<64>(c, P, lp, neg, count, obf, r, rng_key, nonce, C, sign, (hipStream_t)stream);
+  }
   if (c->L2 == 128) return launch_encrypt<128>(c, P, lp, neg, count, obf, r, rng_key, nonce, C, sign, (hipStream_t)stream);
   return launch_encrypt<64>(c, P, lp, neg, count, obf, r, rng_key, nonce, C, sign, (hipStream_t)stream);
 }
@@ -1087,6 +1266,10 @@ fphe_status fphe_decrypt(fphe_ctx* c, const uint32_t* C, size_t count, uint32_t*
   if (!C || !P) return FPHE_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DevGuard g(c->device);
+  if (c->r27) {
+    if (c->L2 == 128) return launch_decrypt27<128>(c, C, count, P, (hipStream_t)stream);
+    return launch_decrypt27<64>(c, C, count, P, (hipStream_t)stream);
+  }
   if (c->L2 == 128) return launch_decrypt<128>(c, C, count, P, (hipStream_t)stream);
   return launch_decrypt<64>(c, C, count, P, (hipStream_t)stream);
 }
@@ -1100,6 +1283,10 @@ fphe_status fphe_add(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, const i
   if (!Ca || !sa || !ea || !Cb || !sb || !eb || !Co || !so || !eo) return FPHE_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DevGuard g(c->device);
+  if (c->r27) {
+    if (c->L2 == 128) return launch_add27<128>(c, Ca, sa, ea, Cb, sb, eb, b_stride, count, Co, so, eo, (hipStream_t)stream);
+    return launch_add27<64>(c, Ca, sa, ea, Cb, sb, eb, b_stride, count, Co, so, eo, (hipStream_t)stream);
+  }
   if (c->L2 == 128) return launch_add<128>(c, Ca, sa, ea, Cb, sb, eb, b_stride, count, Co, so, eo, (hipStream_t)stream);
   return launch_add<64>(c, Ca, sa, ea, Cb, sb, eb, b_stride, count, Co, so, eo, (hipStream_t)stream);
 }
@@ -1113,6 +1300,11 @@ fphe_status fphe_mul(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, const i
   if (!Ca || !sa || !ea || !P || !pneg || !pexp || !Co || !so || !eo || lp == 0) return FPHE_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DevGuard g(c->device);
+  if (c->r27) {
+    if (c->L2 == 128)
+      return launch_mul27<128>(c, Ca, sa, ea, P, lp, pneg, pexp, p_stride, count, Co, so, eo, err, (hipStream_t)stream);
+    return launch_mul27<64>(c, Ca, sa, ea, P, lp, pneg, pexp, p_stride, count, Co, so, eo, err, (hipStream_t)stream);
+  }
   if (c->L2 == 128)
     return launch_mul<128>(c, Ca, sa, ea, P, lp, pneg, pexp, p_stride, count, Co, so, eo, err, (hipStream_t)stream);
   return launch_mul<64>(c, Ca, sa, ea, P, lp, pneg, pexp, p_stride, count, Co, so, eo, err, (hipStream_t)stream);

@@ -1,0 +1,425 @@
+// Reduced-radix (27-bit limb) modexp kernels: encrypt, decrypt (modexp phase), ct-add,
+// ct x pt.  Included by fate_phe.hip after KeyArgs / nude_to_slot / helpers.
+// Geometry: TPI adjacent lanes per element (r27::Geo), E = 64/TPI elements per wave; a
+// wave's E elements always sit in one 64-element memory tile, so the memory tile index is
+// wave-uniform and only the column (element % 64) is per lane.
+#pragma once
+#include "mont27_dev.h"
+
+namespace {
+
+using namespace fphe::r27;
+
+// word w of element column `col` in a tile-major [.][rows][64] u32 tile: per-lane voffset
+__device__ __forceinline__ u32 tld(const __amdgpu_buffer_rsrc_t& r, u32 col, u32 w) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, (col + 64u * w) * 4u, 0, 0);
+}
+__device__ __forceinline__ void tst(const __amdgpu_buffer_rsrc_t& r, u32 col, u32 w, u32 v) {
+  __builtin_amdgcn_raw_buffer_store_b32(v, r, (col + 64u * w) * 4u, 0, 0);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, u32 bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+
+// Words w0 + k of one element column of a tile-major [rows][64] u32 tile.  The descriptor
+// covers exactly the tile, so reads past `rows` return 0 and writes past it are dropped
+// (raw-buffer range check on voffset).  vb is opaque so the per-word addresses stay
+// "vb + const" (folded into the instruction offset) instead of being hoisted as one VGPR
+// per word.
+struct ColIO {
+  __amdgpu_buffer_rsrc_t r;
+  u32 vb;
+  __device__ __forceinline__ u32 ld(int k) const {
+    return __builtin_amdgcn_raw_buffer_load_b32(r, vb + (u32)k * 256u, 0, 0);
+  }
+  __device__ __forceinline__ void st(int k, u32 v) const {
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, vb + (u32)k * 256u, 0, 0);
+  }
+};
+__device__ __forceinline__ ColIO colio(const u32* tile_base, u32 rows, u32 col, u32 w0) {
+  ColIO c;
+  c.r = rsrc(tile_base, rows * 256u);
+  u32 vb = (col + 64u * w0) * 4u;
+  asm volatile("" : "+v"(vb));
+  c.vb = vb;
+  return c;
+}
+
+// Fixed-window modexp with a wave-uniform exponent (27-bit engine).  In: A = X in
+// Montgomery form (< 4N).  Out: X^E in Montgomery form (< 2N).
+template <int TPI, int W>
+__device__ __forceinline__ void powm27(L27& A, u32* bcol, u32 qoff, const Tile& tb, const Mod<TPI>& N,
+                                       u32 np, const u32* __restrict__ Ex, int ebits, int q) {
+  to_slot<TPI>(bcol, qoff, A);
+  tab_store(tb, 1, A);
+#pragma unroll 1
+  for (int k = 2; k < (1 << W); ++k) {
+    mont_mul<TPI>(A, bcol, N, np, q);
+    tab_store(tb, (u32)k, A);
+  }
+  const int nwin = (ebits + W - 1) / W;
+  auto digit = [&](int w) -> u32 {
+    const int b0 = w * W;
+    const int limb = b0 >> 5, off = b0 & 31;
+    u32 v = Ex[limb] >> off;
+    if (off + W > 32) v |= Ex[limb + 1] << (32 - off);
+    return v & ((1u << W) - 1);
+  };
+  tab_load(A, tb, digit(nwin - 1));
+#pragma unroll 1
+  for (int w = nwin - 2; w >= 0; --w) {
+#pragma unroll 1
+    for (int s = 0; s < W; ++s) sqr<TPI>(A, bcol, qoff, N, np, q);
+    const u32 d = digit(w);
+    if (d != 0) {
+      tab_to_slot<TPI>(bcol, qoff, tb, d);
+      mont_mul<TPI>(A, bcol, N, np, q);
+    }
+  }
+}
+
+// ======================================================================================
+// encrypt (27-bit engine): TPI = 4 for 2048-bit keys (n^2: 152 limbs), 2 for 1024-bit.
+// ======================================================================================
+template <int L, int W>
+__global__ __launch_bounds__(kBlock) void k_encrypt27(KeyArgs K, const u32* __restrict__ P, u32 lp,
+                                                      const u8* __restrict__ neg, size_t count, int obf,
+                                                      const u32* __restrict__ rin, u32* __restrict__ Cout,
+                                                      u8* __restrict__ sout, u32* __restrict__ scratch, u32 ldsw) {
+  constexpr int TPI = L / 32;  // 152 limbs for 4096-bit n^2, 76 for 2048-bit
+  using G = Geo<TPI>;
+  constexpr int E = G::E;
+  constexpr u32 L32 = L, L1 = L / 2;
+  extern __shared__ __attribute__((aligned(16))) u32 lds[];
+  G g;
+  const u32 wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u32 gw = blockIdx.x * kWavesPerBlock + wib, nw = gridDim.x * kWavesPerBlock;
+  u32* bcol = lds + wib * ldsw * E + g.e;
+  const u32 qoff = lds_qoff<TPI>(g.q);
+  const Tile tb = make_tile(scratch + (size_t)gw * ((size_t)(1 << W) * LL * FPHE_WAVE), (1u << W) * LL * 256u, g.lane);
+  Mod<TPI> N;
+  N.init(K.N2_27, g.q);
+  const u32 np = K.n2_np27;
+  const u32 nwt = (u32)((count + E - 1) / E);
+  for (u32 wt = gw; wt < nwt; wt += nw) {
+    const size_t ebase = (size_t)wt * E;
+    const u32 tile = (u32)(ebase >> 6);
+    const u32 col = (u32)(ebase & 63) + (u32)g.e;
+    const size_t elem = ebase + g.e;
+    // 1. nude ciphertext 1 + m n (32-bit words) into the LDS tile, rows [0, L32)
+    Tile Pt = make_tile(P + (size_t)tile * lp * FPHE_WAVE, lp * 256u, 0);
+    Pt.vo = col * 4u;
+    bool mneg = false;
+    if (g.q == 0) {
+      mneg = nude_to_slot<L, E>(bcol, K, Pt, lp, neg[elem] != 0);
+      bcol[L * E] = 0;  // the top lane's chunk window reads two words past the number
+      bcol[(L + 1) * E] = 0;
+    }
+    const ColIO Co = colio(Cout + (size_t)tile * L32 * FPHE_WAVE, L32, col, 32u * g.q);
+    L27 A;
+    {
+      const u32* src = bcol + 32 * g.q * E;
+      load_chunk(A, 2u * g.q, [&](int k) { return src[k * E]; });
+    }
+    if (!obf) {
+      normalize_exact<TPI>(A, g.q);
+      store_chunk<TPI>(A, g.q, [&](int k, u32 v) { Co.st(k, v); });
+    } else {
+      tab_store(tb, 0, A);  // C_nude, 27-bit
+      const ColIO Ri = colio(rin + (size_t)tile * L1 * FPHE_WAVE, L1, col, 32u * g.q);
+      load_chunk(A, 2u * g.q, [&](int k) { return Ri.ld(k); });
+      const_to_slot<TPI>(bcol, qoff, K.N2R2_27, g.q);
+      mont_mul<TPI>(A, bcol, N, np, g.q);                                 // r R
+      powm27<TPI, W>(A, bcol, qoff, tb, N, np, K.n, K.nbits, g.q);        // r^n R
+      tab_to_slot<TPI>(bcol, qoff, tb, 0);
+      mont_mul<TPI>(A, bcol, N, np, g.q);                                 // r^n * C_nude (< 2N)
+      finalize<TPI>(A, N, g.q);
+      store_chunk<TPI>(A, g.q, [&](int k, u32 v) { Co.st(k, v); });
+    }
+    if (g.q == 0 && elem < count) sout[elem] = mneg ? 1 : 0;
+  }
+}
+
+// ======================================================================================
+// decrypt, modexp phase: y_s = c^(s-1) mod s^2 for s in {p, q} (paillier/src/lib.rs:174-176,
+// the pow_mod of h_function), written as 32-bit words to Y[tile][2*L1][64] (y_p rows
+// [0,L1), y_q rows [L1, 2L1)).  The CRT tail runs in k_decrypt_crt.
+// ======================================================================================
+template <int TPI, int W>
+__device__ __forceinline__ void dec_half27(const u32* ctile, u32 col, u32 L32, u32* bcol, u32 qoff,
+                                           const Tile& tb, const u32* __restrict__ S2, u32 np,
+                                           const u32* __restrict__ R1, const u32* __restrict__ R2,
+                                           const u32* __restrict__ sm1, int sm1_bits, int q, L27& A) {
+  constexpr int NL = Geo<TPI>::NL;
+  Mod<TPI> N;
+  N.init(S2, q);
+  // c = c_lo + R c_hi (R = 2^(27 NL)):  X = mont(c_lo, R mod s^2) + mont(c_hi, R^2 mod s^2)
+  // = c mod s^2 up to < 4N (c_lo < R against R1 < N, c_hi tiny); then X R via R^2.
+  L27 B;
+  {
+    const u32 bit0 = 27u * NL + 1026u * q;
+    const ColIO Ci = colio(ctile, L32, col, bit0 >> 5);
+    load_chunk(B, bit0 & 31u, [&](int k) { return Ci.ld(k); });
+  }
+  const_to_slot<TPI>(bcol, qoff, R2, q);
+  mont_mul<TPI>(B, bcol, N, np, q);
+  {
+    const ColIO Ci = colio(ctile, L32, col, 32u * q);
+    load_chunk(A, 2u * q, [&](int k) { return Ci.ld(k); });
+  }
+  const_to_slot<TPI>(bcol, qoff, R1, q);
+  mont_mul<TPI>(A, bcol, N, np, q);
+#pragma unroll
+  for (int j = 0; j < LL; ++j) A.set(j, A[j] + B[j]);
+  normalize_exact<TPI>(A, q);  // < 4N, only ever multiplied by R^2 < N next
+  const_to_slot<TPI>(bcol, qoff, R2, q);
+  mont_mul<TPI>(A, bcol, N, np, q);  // c R, < 2N
+  powm27<TPI, W>(A, bcol, qoff, tb, N, np, sm1, sm1_bits, q);
+  one_to_slot<TPI>(bcol, qoff, q);
+  mont_mul<TPI>(A, bcol, N, np, q);  // y = c^(s-1) mod s^2 (< 2N)
+  finalize<TPI>(A, N, q);
+}
+
+template <int L, int W>
+__global__ __launch_bounds__(kBlock) void k_decrypt_pow27(KeyArgs K, const u32* __restrict__ C, size_t count,
+                                                          u32* __restrict__ Y, u32* __restrict__ scratch, u32 ldsw) {
+  constexpr int TPI = L / 64;  // p^2, q^2: 76 limbs for 2048-bit keys, 38 for 1024-bit
+  using G = Geo<TPI>;
+  constexpr int E = G::E;
+  constexpr u32 L32 = L, L1 = L / 2;
+  extern __shared__ __attribute__((aligned(16))) u32 lds[];
+  G g;
+  const u32 wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u32 gw = blockIdx.x * kWavesPerBlock + wib, nw = gridDim.x * kWavesPerBlock;
+  u32* bcol = lds + wib * ldsw * E + g.e;
+  const u32 qoff = lds_qoff<TPI>(g.q);
+  const Tile tb = make_tile(scratch + (size_t)gw * ((size_t)(1 << W) * LL * FPHE_WAVE), (1u << W) * LL * 256u, g.lane);
+  const u32 nwt = (u32)((count + E - 1) / E);
+  for (u32 wt = gw; wt < nwt; wt += nw) {
+    const size_t ebase = (size_t)wt * E;
+    const u32 tile = (u32)(ebase >> 6);
+    const u32 col = (u32)(ebase & 63) + (u32)g.e;
+    const u32* ctile = C + (size_t)tile * L32 * FPHE_WAVE;
+    u32* ytile = Y + (size_t)tile * 2 * L1 * FPHE_WAVE;
+    L27 A;
+    dec_half27<TPI, W>(ctile, col, L32, bcol, qoff, tb, K.P2_27, K.p2_np27, K.P2R1_27, K.P2R2_27, K.pm1,
+                       K.pm1_bits, g.q, A);
+    {
+      const ColIO Yo = colio(ytile, 2 * L1, col, 32u * g.q);
+      store_chunk<TPI>(A, g.q, [&](int k, u32 v) { Yo.st(k, v); });
+    }
+    dec_half27<TPI, W>(ctile, col, L32, bcol, qoff, tb, K.Q2_27, K.q2_np27, K.Q2R1_27, K.Q2R2_27, K.qm1,
+                       K.qm1_bits, g.q, A);
+    {
+      const ColIO Yo = colio(ytile, 2 * L1, col, L1 + 32u * g.q);
+      store_chunk<TPI>(A, g.q, [&](int k, u32 v) { Yo.st(k, v); });
+    }
+  }
+}
+
+// ======================================================================================
+// ct-add (fixedpoint_paillier/src/lib.rs:301-333), 27-bit engine
+// ======================================================================================
+template <int L>
+__global__ __launch_bounds__(kBlock) void k_add27(KeyArgs K, const u32* __restrict__ Ca, const u8* __restrict__ sa,
+                                                  const int32_t* __restrict__ ea, const u32* __restrict__ Cb,
+                                                  const u8* __restrict__ sb, const int32_t* __restrict__ eb,
+                                                  int bstride, size_t count, u32* __restrict__ Co,
+                                                  u8* __restrict__ so, int32_t* __restrict__ eo, u32 ldsw) {
+  constexpr int TPI = L / 32;
+  using G = Geo<TPI>;
+  constexpr int E = G::E;
+  constexpr u32 L32 = L;
+  extern __shared__ __attribute__((aligned(16))) u32 lds[];
+  G g;
+  const u32 wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u32 gw = blockIdx.x * kWavesPerBlock + wib, nw = gridDim.x * kWavesPerBlock;
+  u32* bcol = lds + wib * ldsw * E + g.e;
+  const u32 qoff = lds_qoff<TPI>(g.q);
+  Mod<TPI> N;
+  N.init(K.N2_27, g.q);
+  const u32 np = K.n2_np27;
+  const u32 nwt = (u32)((count + E - 1) / E);
+  for (u32 wt = gw; wt < nwt; wt += nw) {
+    const size_t ebase = (size_t)wt * E;
+    const u32 tile = (u32)(ebase >> 6);
+    const u32 col = (u32)(ebase & 63) + (u32)g.e;
+    const size_t elem = ebase + g.e;
+    const size_t be = bstride ? elem : 0;
+    const u32 bcolm = bstride ? col : 0u;
+    const ColIO Ai = colio(Ca + (size_t)tile * L32 * FPHE_WAVE, L32, col, 32u * g.q);
+    const ColIO Bi = colio(bstride ? Cb + (size_t)tile * L32 * FPHE_WAVE : Cb, L32, bcolm, 32u * g.q);
+    const ColIO Oo = colio(Co + (size_t)tile * L32 * FPHE_WAVE, L32, col, 32u * g.q);
+    const int xa = ea[elem], xb = eb[be];
+    const u32 sav = sa[elem], sbv = sb[be];
+    const bool x_is_a = xa > xb;
+    L27 A, Bv;
+    load_chunk(A, 2u * g.q, [&](int k) { return Ai.ld(k); });
+    load_chunk(Bv, 2u * g.q, [&](int k) { return Bi.ld(k); });
+    // literal-1 tests (:303-308) over the element's lanes
+    u32 za = 0, zb = 0;
+#pragma unroll
+    for (int j = 0; j < LL; ++j) {
+      const u32 one = (j == 0 && g.q == 0) ? 1u : 0u;
+      za |= A[j] ^ one;
+      zb |= Bv[j] ^ one;
+    }
+    za = elem_or<TPI>(za);
+    zb = elem_or<TPI>(zb);
+    const bool lit_a = za == 0 && sav == 0;
+    const bool lit_b = zb == 0 && sbv == 0;
+    int d = x_is_a ? xa - xb : xb - xa;
+    if (lit_a || lit_b) d = 0;
+    // x = higher-exp operand (stays in A), y = the other (to LDS at the end)
+#pragma unroll
+    for (int j = 0; j < LL; ++j) {
+      const u32 xv = x_is_a ? A[j] : Bv[j];
+      const u32 yv = x_is_a ? Bv[j] : A[j];
+      A.set(j, xv);
+      Bv.set(j, yv);
+    }
+    const_to_slot<TPI>(bcol, qoff, K.N2R2_27, g.q);
+    mont_mul<TPI>(A, bcol, N, np, g.q);  // x R
+    const int nsq = wave_max_int(4 * d);
+#pragma unroll 1
+    for (int k = 0; k < nsq; ++k) {
+      if (k < 4 * d) sqr<TPI>(A, bcol, qoff, N, np, g.q);
+    }
+    to_slot<TPI>(bcol, qoff, Bv);
+    mont_mul<TPI>(A, bcol, N, np, g.q);  // x^(16^d) y mod n^2 (< 2N)
+    finalize<TPI>(A, N, g.q);
+    const u32 sy = x_is_a ? sbv : sav;
+    u32 sign = d == 0 ? (sav ^ sbv) : sy;
+    int exo = xa < xb ? xa : xb;
+    if (lit_a || lit_b) {
+      // copy the other operand through untouched (words, not limbs: no re-encoding)
+      sign = lit_a ? sbv : sav;
+      exo = lit_a ? xb : xa;
+    }
+    if (lit_a || lit_b) {
+#pragma unroll
+      for (int k = 0; k < 32; ++k) Oo.st(k, lit_a ? Bi.ld(k) : Ai.ld(k));
+    } else {
+      store_chunk<TPI>(A, g.q, [&](int k, u32 v) { Oo.st(k, v); });
+    }
+    if (g.q == 0 && elem < count) {
+      so[elem] = (u8)sign;
+      eo[elem] = exo;
+    }
+  }
+}
+
+// ======================================================================================
+// ct x pt (fixedpoint_paillier/src/lib.rs:334-349), 27-bit engine, per-element exponents
+// ======================================================================================
+template <int L, int W>
+__global__ __launch_bounds__(kBlock) void k_mul27(KeyArgs K, const u32* __restrict__ Ca, const u8* __restrict__ sa,
+                                                  const int32_t* __restrict__ ea, const u32* __restrict__ P, u32 lp,
+                                                  const u8* __restrict__ pneg, const int32_t* __restrict__ pexp,
+                                                  int pstride, size_t count, u32* __restrict__ Co,
+                                                  u8* __restrict__ so, int32_t* __restrict__ eo,
+                                                  int32_t* __restrict__ err, u32* __restrict__ scratch, u32 ldsw) {
+  constexpr int TPI = L / 32;
+  using G = Geo<TPI>;
+  constexpr int E = G::E;
+  constexpr u32 L32 = L, L1 = L / 2;
+  extern __shared__ __attribute__((aligned(16))) u32 lds[];
+  G g;
+  const u32 wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u32 gw = blockIdx.x * kWavesPerBlock + wib, nw = gridDim.x * kWavesPerBlock;
+  u32* bcol = lds + wib * ldsw * E + g.e;
+  const u32 qoff = lds_qoff<TPI>(g.q);
+  const Tile tb = make_tile(scratch + (size_t)gw * ((size_t)(1 << W) * LL * FPHE_WAVE), (1u << W) * LL * 256u, g.lane);
+  Mod<TPI> N;
+  N.init(K.N2_27, g.q);
+  const u32 np = K.n2_np27;
+  const u32 nwt = (u32)((count + E - 1) / E);
+  for (u32 wt = gw; wt < nwt; wt += nw) {
+    const size_t ebase = (size_t)wt * E;
+    const u32 tile = (u32)(ebase >> 6);
+    const u32 col = (u32)(ebase & 63) + (u32)g.e;
+    const size_t elem = ebase + g.e;
+    const size_t pe = pstride ? elem : 0;
+    const u32 pcol = pstride ? col : 0u;
+    const __amdgpu_buffer_rsrc_t Pr = pstride ? rsrc(P + (size_t)tile * lp * FPHE_WAVE, lp * 256u) : rsrc(P, lp * 256u);
+    const ColIO Ai = colio(Ca + (size_t)tile * L32 * FPHE_WAVE, L32, col, 32u * g.q);
+    const ColIO Oo = colio(Co + (size_t)tile * L32 * FPHE_WAVE, L32, col, 32u * g.q);
+    // classify the significand (:335-344); every lane of the element does the same scan
+    u32 any = 0;
+    int ebits = 0;
+    u32 br_max = 0, br_nmm = 0;
+#pragma unroll 4
+    for (u32 j = 0; j < L1; ++j) {
+      const u32 pj = j < lp ? tld(Pr, pcol, j) : 0u;
+      any |= pj;
+      if (pj) ebits = 32 * (int)j + 32 - __clz(pj);
+      const u64 d1 = (u64)K.max_int[j] - pj - br_max;
+      br_max = (u32)(d1 >> 63);
+      const u64 d2 = (u64)pj - K.n_mm[j] - br_nmm;
+      br_nmm = (u32)(d2 >> 63);
+    }
+    const bool isneg = (pneg[pe] != 0) && (any != 0);
+    const bool big = !isneg && (br_nmm == 0);
+    const bool invalid = !isneg && !big && (br_max != 0);
+    u32 ef = 0;
+    if (isneg || big) ef |= FPHE_EF_NOT_INVERTIBLE;
+    if (invalid) ef |= FPHE_EF_MUL_INVALID_PT;
+    if (g.q == 0 && elem < count) set_err(err, ef);
+    if (isneg || big || invalid) ebits = 0;
+    const int maxbits = wave_max_int(ebits);
+    L27 A;
+    load_chunk(A, 2u * g.q, [&](int k) { return Ai.ld(k); });
+    const_to_slot<TPI>(bcol, qoff, K.N2R2_27, g.q);
+    mont_mul<TPI>(A, bcol, N, np, g.q);  // X = c R
+    if (maxbits > 0) {
+      to_slot<TPI>(bcol, qoff, A);
+      tab_store(tb, 1, A);
+      {
+        L27 one;
+#pragma unroll
+        for (int j = 0; j < LL; ++j) one.set(j, K.N2R1_27[g.q * LL + j]);
+        tab_store(tb, 0, one);  // Montgomery 1
+      }
+#pragma unroll 1
+      for (int k = 2; k < (1 << W); ++k) {
+        mont_mul<TPI>(A, bcol, N, np, g.q);
+        tab_store(tb, (u32)k, A);
+      }
+      const int nwin = (maxbits + W - 1) / W;
+      auto digit = [&](int wi) -> u32 {
+        const int b0 = wi * W;
+        const u32 limb = (u32)(b0 >> 5);
+        const u32 v = limb < lp ? tld(Pr, pcol, limb) : 0u;
+        const u32 dd = (v >> (b0 & 31)) & ((1u << W) - 1);
+        return ebits == 0 ? 0u : dd;
+      };
+      auto entry_tile = [&](u32 dgt) {  // per-lane entry through the lane-varying voffset
+        Tile t = tb;
+        t.vo = tb.vo + dgt * LL * 256u;
+        return t;
+      };
+      tab_load(A, entry_tile(digit(nwin - 1)), 0);
+#pragma unroll 1
+      for (int wi = nwin - 2; wi >= 0; --wi) {
+#pragma unroll 1
+        for (int s = 0; s < W; ++s) sqr<TPI>(A, bcol, qoff, N, np, g.q);
+        tab_to_slot<TPI>(bcol, qoff, entry_tile(digit(wi)), 0);
+        mont_mul<TPI>(A, bcol, N, np, g.q);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < LL; ++j) A.set(j, K.N2R1_27[g.q * LL + j]);
+    }
+    one_to_slot<TPI>(bcol, qoff, g.q);
+    mont_mul<TPI>(A, bcol, N, np, g.q);  // leave Montgomery form (<= N)
+    finalize<TPI>(A, N, g.q);
+    store_chunk<TPI>(A, g.q, [&](int k, u32 v) { Oo.st(k, v); });
+    if (g.q == 0 && elem < count) {
+      so[elem] = 0;
+      eo[elem] = ea[elem] + pexp[pe];
+    }
+  }
+}
+
+}  // namespace
