@@ -8,6 +8,7 @@
 #include <stdint.h>
 #include <string.h>
 #include <stdlib.h>
+#include <stdio.h>
 #include <vector>
 #include <mutex>
 
@@ -838,12 +839,15 @@ Limbs to27(const Limbs& v, int nl) {
 }
 
 template <typename KernT>
-unsigned occ_grid(const fphe_ctx* c, KernT k, size_t lds, size_t waves) {
+unsigned occ_grid(const fphe_ctx* c, KernT k, size_t lds, size_t waves, const char* what = "") {
   int nb = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kBlock, lds) != hipSuccess || nb < 1) nb = 1;
   size_t g = (size_t)c->cus * (size_t)nb;
   const size_t need = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
   if (need < g) g = need;
+  if (getenv("FPHE_DEBUG"))
+    fprintf(stderr, "[fphe] %s: occupancy api %d blocks/CU, lds %zu B/block, grid %zu blocks for %zu waves\n", what, nb,
+            lds, g, waves);
   return (unsigned)(g ? g : 1);
 }
 
@@ -978,7 +982,7 @@ fphe_status launch_encrypt27(fphe_ctx* c, const uint32_t* P, uint32_t lp, const 
   auto kern = k_encrypt27<L, kWinEnc>;
   const size_t lds = (size_t)kWavesPerBlock * LDSW * E * 4;
   set_lds(kern, lds);
-  const unsigned grid = occ_grid(c, kern, lds, (count + E - 1) / E);
+  const unsigned grid = occ_grid(c, kern, lds, (count + E - 1) / E, "encrypt27");
   const size_t tbytes = (size_t)grid * kWavesPerBlock * (1u << kWinEnc) * r27::LL * FPHE_WAVE * 4;
   const size_t rbytes = (size_t)ntiles_of(count) * L1 * FPHE_WAVE * 4;
   const bool draw = obf && !r;
@@ -1003,7 +1007,7 @@ fphe_status launch_decrypt27(fphe_ctx* c, const uint32_t* C, size_t count, uint3
   auto kern = k_decrypt_pow27<L, kWinEnc>;
   const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
   set_lds(kern, lds);
-  const unsigned grid = occ_grid(c, kern, lds, (count + E - 1) / E);
+  const unsigned grid = occ_grid(c, kern, lds, (count + E - 1) / E, "decrypt_pow27");
   const size_t tbytes = (size_t)grid * kWavesPerBlock * (1u << kWinEnc) * r27::LL * FPHE_WAVE * 4;
   const size_t ybytes = (size_t)ntiles_of(count) * 2 * LH * FPHE_WAVE * 4;
   if (ensure_scratch(c, tbytes + ybytes) != FPHE_OK) return FPHE_ERR_HIP;

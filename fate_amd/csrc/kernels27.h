@@ -152,8 +152,12 @@ __device__ __forceinline__ void dec_half27(const u32* ctile, u32 col, u32 L32, u
                                            const u32* __restrict__ R1, const u32* __restrict__ R2,
                                            const u32* __restrict__ sm1, int sm1_bits, int q, L27& A) {
   constexpr int NL = Geo<TPI>::NL;
+  // opaque modulus pointer: keeps LICM from hoisting both halves' limbs (p^2 and q^2) out
+  // of the element loop, which would hold 2 x 38 VGPRs for the whole kernel
+  const u32* S2o = S2;
+  asm volatile("" : "+s"(S2o));
   Mod<TPI> N;
-  N.init(S2, q);
+  N.init(S2o, q);
   // c = c_lo + R c_hi (R = 2^(27 NL)):  X = mont(c_lo, R mod s^2) + mont(c_hi, R^2 mod s^2)
   // = c mod s^2 up to < 4N (c_lo < R against R1 < N, c_hi tiny); then X R via R^2.
   L27 B;
@@ -164,12 +168,14 @@ __device__ __forceinline__ void dec_half27(const u32* ctile, u32 col, u32 L32, u
   }
   const_to_slot<TPI>(bcol, qoff, R2, q);
   mont_mul<TPI>(B, bcol, N, np, q);
+  tab_store(tb, 0, B);  // parked in the (otherwise unused) table entry 0, not in registers
   {
     const ColIO Ci = colio(ctile, L32, col, 32u * q);
     load_chunk(A, 2u * q, [&](int k) { return Ci.ld(k); });
   }
   const_to_slot<TPI>(bcol, qoff, R1, q);
   mont_mul<TPI>(A, bcol, N, np, q);
+  tab_load(B, tb, 0);
 #pragma unroll
   for (int j = 0; j < LL; ++j) A.set(j, A[j] + B[j]);
   normalize_exact<TPI>(A, q);  // < 4N, only ever multiplied by R^2 < N next
@@ -271,14 +277,10 @@ __global__ __launch_bounds__(kBlock) void k_add27(KeyArgs K, const u32* __restri
     const bool lit_b = zb == 0 && sbv == 0;
     int d = x_is_a ? xa - xb : xb - xa;
     if (lit_a || lit_b) d = 0;
-    // x = higher-exp operand (stays in A), y = the other (to LDS at the end)
+    // x = higher-exp operand (stays in A); y is re-read at the end rather than held in
+    // registers across the squarings
 #pragma unroll
-    for (int j = 0; j < LL; ++j) {
-      const u32 xv = x_is_a ? A[j] : Bv[j];
-      const u32 yv = x_is_a ? Bv[j] : A[j];
-      A.set(j, xv);
-      Bv.set(j, yv);
-    }
+    for (int j = 0; j < LL; ++j) A.set(j, x_is_a ? A[j] : Bv[j]);
     const_to_slot<TPI>(bcol, qoff, K.N2R2_27, g.q);
     mont_mul<TPI>(A, bcol, N, np, g.q);  // x R
     const int nsq = wave_max_int(4 * d);
@@ -286,6 +288,7 @@ __global__ __launch_bounds__(kBlock) void k_add27(KeyArgs K, const u32* __restri
     for (int k = 0; k < nsq; ++k) {
       if (k < 4 * d) sqr<TPI>(A, bcol, qoff, N, np, g.q);
     }
+    load_chunk(Bv, 2u * g.q, [&](int k) { return x_is_a ? Bi.ld(k) : Ai.ld(k); });
     to_slot<TPI>(bcol, qoff, Bv);
     mont_mul<TPI>(A, bcol, N, np, g.q);  // x^(16^d) y mod n^2 (< 2N)
     finalize<TPI>(A, N, g.q);
