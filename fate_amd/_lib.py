@@ -30,7 +30,7 @@ EF_NOT_INVERTIBLE = 0x10
 EXPORTED_SYMBOLS = (
     "fphe_ctx_create", "fphe_ctx_destroy", "fphe_ctx_limbs",
     "fphe_encode_f32", "fphe_encode_f64", "fphe_decode_f32", "fphe_decode_f64",
-    "fphe_encrypt", "fphe_decrypt", "fphe_add", "fphe_mul",
+    "fphe_encrypt", "fphe_decrypt", "fphe_add", "fphe_mul", "fphe_neg", "fphe_sqmul",
 )
 
 _lock = threading.Lock()
@@ -79,6 +79,10 @@ def load() -> ctypes.CDLL:
         lib.fphe_mul.argtypes = [vp, vp, vp, vp, vp, ctypes.c_uint32, vp, vp, ctypes.c_int, ctypes.c_size_t,
                                  vp, vp, vp, vp, vp]
         lib.fphe_mul.restype = st
+        lib.fphe_neg.argtypes = [vp, vp, ctypes.c_size_t, vp, vp, vp]
+        lib.fphe_neg.restype = st
+        lib.fphe_sqmul.argtypes = [vp, vp, vp, vp, ctypes.c_uint32, ctypes.c_size_t, vp, vp, vp]
+        lib.fphe_sqmul.restype = st
         _lib = lib
         return lib
 

@@ -49,6 +49,8 @@ struct KeyArgs {
   const u32* P2_27; const u32* P2R1_27; const u32* P2R2_27;  // p^2 ...                      [NLh]
   const u32* Q2_27; const u32* Q2R1_27; const u32* Q2R2_27;
   u32 n2_np27, p2_np27, q2_np27;                             // -N^{-1} mod 2^27
+  const u32* Nn_27; const u32* NnR1_27; const u32* NnR2_27;  // n, R mod n, R^2 mod n    [NLh]
+  u32 nn_np27, nn_inv27;                                     // -n^{-1}, n^{-1} mod 2^27
 };
 
 __device__ __forceinline__ void set_err(int32_t* err, u32 f) {
@@ -1036,18 +1038,65 @@ fphe_status launch_add27(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, con
 }
 
 template <int L>
+fphe_status launch_sqmul27(fphe_ctx* c, const uint32_t* Ca, const uint32_t* Cb, const uint8_t* sb, int nsq,
+                           size_t count, uint32_t* Co, uint8_t* so, hipStream_t s) {
+  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = r27::LL * TPI;
+  auto kern = k_sqmul27<L>;
+  const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
+  set_lds(kern, lds);
+  const unsigned grid = occ_grid(c, kern, lds, (count + E - 1) / E, "sqmul27");
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, Ca, Cb, sb, nsq, count, Co, so, (u32)NL);
+  return hip_ok(hipGetLastError());
+}
+
+// X0: scratch of ntiles * L1 * 64 words (the mod-n inverses between the two kernels)
+template <int L>
+void launch_inv27(fphe_ctx* c, const uint32_t* Ca, size_t count, const uint8_t* need, uint32_t* Co,
+                  int32_t* err, u32* X0, hipStream_t s) {
+  constexpr int TPIh = L / 64, Eh = FPHE_WAVE / TPIh, NLh = r27::LL * TPIh, L1 = L / 2;
+  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = r27::LL * TPI;
+  auto k1 = k_inv_n27<L>;
+  const size_t lds1 = (size_t)kWavesPerBlock * NLh * Eh * 4;
+  set_lds(k1, lds1);
+  const unsigned g1 = occ_grid(c, k1, lds1, (count + Eh - 1) / Eh, "inv_n27");
+  (void)L1;
+  hipLaunchKernelGGL(k1, dim3(g1), dim3(kBlock), lds1, s, c->K, Ca, count, need, X0, err, (u32)NLh);
+  auto k2 = k_inv_lift27<L>;
+  const size_t lds2 = (size_t)kWavesPerBlock * NL * E * 4;
+  set_lds(k2, lds2);
+  const unsigned g2 = occ_grid(c, k2, lds2, (count + E - 1) / E, "inv_lift27");
+  hipLaunchKernelGGL(k2, dim3(g2), dim3(kBlock), lds2, s, c->K, Ca, count, need, X0, Co, (u32)NL);
+}
+
+template <int L>
 fphe_status launch_mul27(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, const int32_t* ea, const uint32_t* P,
                          uint32_t lp, const uint8_t* pneg, const int32_t* pexp, int pstride, size_t count,
                          uint32_t* Co, uint8_t* so, int32_t* eo, int32_t* err, hipStream_t s) {
-  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = r27::LL * TPI;
+  (void)sa;  // powm results are canonical whatever the base's sign (lib.rs:334-349)
+  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = r27::LL * TPI, L1 = L / 2;
   auto kern = k_mul27<L, kWinMul>;
   const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
   set_lds(kern, lds);
-  const unsigned grid = occ_grid(c, kern, lds, (count + E - 1) / E);
+  const unsigned grid = occ_grid(c, kern, lds, (count + E - 1) / E, "mul27");
+  // scratch: [window tables][need T*64 B][ebits T*64 i32][E T*L1*64 w][Cinv T*L*64 w][X0 T*L1*64 w]
+  const size_t nt = ntiles_of(count);
   const size_t tbytes = (size_t)grid * kWavesPerBlock * (1u << kWinMul) * r27::LL * FPHE_WAVE * 4;
-  if (ensure_scratch(c, tbytes) != FPHE_OK) return FPHE_ERR_HIP;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, Ca, sa, ea, P, lp, pneg, pexp, pstride, count, Co,
-                     so, eo, err, c->scratch, (u32)NL);
+  const size_t o_need = tbytes, o_eb = o_need + nt * FPHE_WAVE, o_E = o_eb + nt * FPHE_WAVE * 4;
+  const size_t o_inv = o_E + nt * L1 * FPHE_WAVE * 4, o_x0 = o_inv + nt * L * FPHE_WAVE * 4;
+  const size_t total = o_x0 + nt * L1 * FPHE_WAVE * 4;
+  if (ensure_scratch(c, total) != FPHE_OK) return FPHE_ERR_HIP;
+  char* base = reinterpret_cast<char*>(c->scratch);
+  u8* need = reinterpret_cast<u8*>(base + o_need);
+  int32_t* eb = reinterpret_cast<int32_t*>(base + o_eb);
+  u32* Ex = reinterpret_cast<u32*>(base + o_E);
+  u32* Cinv = reinterpret_cast<u32*>(base + o_inv);
+  u32* X0 = reinterpret_cast<u32*>(base + o_x0);
+  const unsigned pgrid = (unsigned)std::min<size_t>((count + 255) / 256, (size_t)c->cus * 8);
+  hipLaunchKernelGGL(k_mul_prep<L>, dim3(pgrid), dim3(256), 0, s, c->K, P, lp, pneg, pstride, count, need, Ex, eb,
+                     err);
+  launch_inv27<L>(c, Ca, count, need, Cinv, err, X0, s);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, Ca, Cinv, need, ea, Ex, eb, pexp, pstride, count,
+                     Co, so, eo, c->scratch, (u32)NL);
   return hip_ok(hipGetLastError());
 }
 
@@ -1090,6 +1139,9 @@ fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, 
     const size_t o_N2_27 = put(to27(N2, NL2), NL2);
     const size_t o_N2R1_27 = put(to27(hbn::pow2_mod((size_t)27 * NL2, N2), NL2), NL2);
     const size_t o_N2R2_27 = put(to27(hbn::pow2_mod((size_t)54 * NL2, N2), NL2), NL2);
+    const size_t o_Nn_27 = put(to27(n, NLh), NLh);
+    const size_t o_NnR1_27 = put(to27(hbn::pow2_mod((size_t)27 * NLh, n), NLh), NLh);
+    const size_t o_NnR2_27 = put(to27(hbn::pow2_mod((size_t)54 * NLh, n), NLh), NLh);
     size_t o_P2_27 = 0, o_P2R1_27 = 0, o_P2R2_27 = 0, o_Q2_27 = 0, o_Q2R1_27 = 0, o_Q2R2_27 = 0;
     size_t o_P2 = 0, o_P2R3 = 0, o_pm1 = 0, o_p = 0, o_pinv2 = 0, o_hpR = 0;
     size_t o_Q2 = 0, o_Q2R3 = 0, o_qm1 = 0, o_q = 0, o_qinv2 = 0, o_hqR = 0, o_pinvqR = 0;
@@ -1153,6 +1205,9 @@ fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, 
     K.nbits = (int)key_bits;
     K.N2_27 = b + o_N2_27; K.N2R1_27 = b + o_N2R1_27; K.N2R2_27 = b + o_N2R2_27;
     K.n2_np27 = K.n2_n0inv & ((1u << 27) - 1u);
+    K.Nn_27 = b + o_Nn_27; K.NnR1_27 = b + o_NnR1_27; K.NnR2_27 = b + o_NnR2_27;
+    K.nn_np27 = hbn::neg_inv32(n[0]) & ((1u << 27) - 1u);
+    K.nn_inv27 = (0u - hbn::neg_inv32(n[0])) & ((1u << 27) - 1u);
     {
       const char* eng = getenv("FPHE_ENGINE");
       c->r27 = !(eng && strcmp(eng, "32") == 0);
@@ -1293,6 +1348,32 @@ fphe_status fphe_add(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, const i
   }
   if (c->L2 == 128) return launch_add<128>(c, Ca, sa, ea, Cb, sb, eb, b_stride, count, Co, so, eo, (hipStream_t)stream);
   return launch_add<64>(c, Ca, sa, ea, Cb, sb, eb, b_stride, count, Co, so, eo, (hipStream_t)stream);
+}
+
+
+fphe_status fphe_neg(fphe_ctx* c, const uint32_t* Ca, size_t count, uint32_t* Co, int32_t* err, void* stream) {
+  if (!c || !err) return FPHE_ERR_ARG;
+  if (count == 0) return FPHE_OK;
+  if (!Ca || !Co) return FPHE_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DevGuard g(c->device);
+  const size_t xbytes = (size_t)ntiles_of(count) * c->L1 * FPHE_WAVE * 4;
+  if (ensure_scratch(c, xbytes) != FPHE_OK) return FPHE_ERR_HIP;
+  if (c->L2 == 128) launch_inv27<128>(c, Ca, count, nullptr, Co, err, c->scratch, (hipStream_t)stream);
+  else launch_inv27<64>(c, Ca, count, nullptr, Co, err, c->scratch, (hipStream_t)stream);
+  return hip_ok(hipGetLastError());
+}
+
+
+fphe_status fphe_sqmul(fphe_ctx* c, const uint32_t* Ca, const uint32_t* Cb, const uint8_t* sb, uint32_t nsq,
+                       size_t count, uint32_t* Co, uint8_t* so, void* stream) {
+  if (!c) return FPHE_ERR_ARG;
+  if (count == 0) return FPHE_OK;
+  if (!Ca || !Cb || !sb || !Co || !so || nsq > (1u << 20)) return FPHE_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DevGuard g(c->device);
+  if (c->L2 == 128) return launch_sqmul27<128>(c, Ca, Cb, sb, (int)nsq, count, Co, so, (hipStream_t)stream);
+  return launch_sqmul27<64>(c, Ca, Cb, sb, (int)nsq, count, Co, so, (hipStream_t)stream);
 }
 
 

@@ -5,6 +5,7 @@
 // wave-uniform and only the column (element % 64) is per lane.
 #pragma once
 #include "mont27_dev.h"
+#include "inv27.h"
 
 namespace {
 
@@ -314,15 +315,72 @@ __global__ __launch_bounds__(kBlock) void k_add27(KeyArgs K, const u32* __restri
 }
 
 // ======================================================================================
-// ct x pt (fixedpoint_paillier/src/lib.rs:334-349), 27-bit engine, per-element exponents
+// ct x pt (fixedpoint_paillier/src/lib.rs:334-349), 27-bit engine, per-element exponents.
+// k_mul_prep classifies each plaintext significand as the reference does:
+//   pt >= n - max_int ("big", an encoded negative int): c^-1 ^ (n - pt)
+//   pt <= max_int, negative float significand:           c^-1 ^ |pt|  (GMP powm, negative exp)
+//   pt <= max_int otherwise:                              c ^ pt
+//   else: panic "invalid plaintext"
+// and writes need-inverse flags, the exponent magnitude E [T][L1][64] and its bit length.
+// ======================================================================================
+template <int L>
+__global__ __launch_bounds__(256) void k_mul_prep(KeyArgs K, const u32* __restrict__ P, u32 lp,
+                                                  const u8* __restrict__ pneg, int pstride, size_t count,
+                                                  u8* __restrict__ need, u32* __restrict__ Eout,
+                                                  int32_t* __restrict__ ebits_out, int32_t* __restrict__ err) {
+  constexpr int L1 = L / 2;
+  u32 ef = 0;
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < count; e += (size_t)gridDim.x * blockDim.x) {
+    const size_t pe = pstride ? e : 0;
+    u32 M[L1];
+    u32 any = 0, br_max = 0, br_nmm = 0;
+#pragma unroll
+    for (int j = 0; j < L1; ++j) {
+      M[j] = (u32)j < lp ? P[tiled(pe, lp, (u32)j)] : 0u;
+      any |= M[j];
+      const u64 d1 = (u64)K.max_int[j] - M[j] - br_max;
+      br_max = (u32)(d1 >> 63);
+      const u64 d2 = (u64)M[j] - K.n_mm[j] - br_nmm;
+      br_nmm = (u32)(d2 >> 63);
+    }
+    u32 hi = 0;
+    for (u32 j = L1; j < lp; ++j) hi |= P[tiled(pe, lp, j)];
+    // negative significand: always powm(c^-1, |sig|) (a negative sig is <= max_int)
+    const bool isneg = (pneg[pe] != 0) && (any != 0);
+    bool big = !isneg && (br_nmm == 0) && hi == 0;  // P >= n - max_int
+    bool invalid = hi != 0 || (!isneg && !big && br_max != 0);
+    if (big) {  // exponent n - P (P > n would need a negative exponent: unreachable for encodings)
+      u32 br = 0;
+#pragma unroll
+      for (int j = 0; j < L1; ++j) {
+        const u64 d = (u64)K.n[j] - M[j] - br;
+        M[j] = (u32)d;
+        br = (u32)(d >> 63);
+      }
+      if (br) invalid = true;
+    }
+    int eb = 0;
+#pragma unroll
+    for (int j = 0; j < L1; ++j) {
+      if (invalid) M[j] = 0;
+      if (M[j]) eb = 32 * j + 32 - __clz(M[j]);
+      Eout[tiled(e, L1, (u32)j)] = M[j];
+    }
+    if (invalid) ef |= FPHE_EF_MUL_INVALID_PT;
+    need[e] = (isneg || big) && !invalid ? 1 : 0;
+    ebits_out[e] = eb;
+  }
+  set_err(err, ef);
+}
+
 // ======================================================================================
 template <int L, int W>
-__global__ __launch_bounds__(kBlock) void k_mul27(KeyArgs K, const u32* __restrict__ Ca, const u8* __restrict__ sa,
-                                                  const int32_t* __restrict__ ea, const u32* __restrict__ P, u32 lp,
-                                                  const u8* __restrict__ pneg, const int32_t* __restrict__ pexp,
-                                                  int pstride, size_t count, u32* __restrict__ Co,
-                                                  u8* __restrict__ so, int32_t* __restrict__ eo,
-                                                  int32_t* __restrict__ err, u32* __restrict__ scratch, u32 ldsw) {
+__global__ __launch_bounds__(kBlock) void k_mul27(KeyArgs K, const u32* __restrict__ Ca, const u32* __restrict__ Cinv,
+                                                  const u8* __restrict__ need, const int32_t* __restrict__ ea,
+                                                  const u32* __restrict__ Ex, const int32_t* __restrict__ ebits_in,
+                                                  const int32_t* __restrict__ pexp, int pstride, size_t count,
+                                                  u32* __restrict__ Co, u8* __restrict__ so, int32_t* __restrict__ eo,
+                                                  u32* __restrict__ scratch, u32 ldsw) {
   constexpr int TPI = L / 32;
   using G = Geo<TPI>;
   constexpr int E = G::E;
@@ -343,38 +401,19 @@ __global__ __launch_bounds__(kBlock) void k_mul27(KeyArgs K, const u32* __restri
     const u32 tile = (u32)(ebase >> 6);
     const u32 col = (u32)(ebase & 63) + (u32)g.e;
     const size_t elem = ebase + g.e;
+    const bool inside = elem < count;
     const size_t pe = pstride ? elem : 0;
-    const u32 pcol = pstride ? col : 0u;
-    const __amdgpu_buffer_rsrc_t Pr = pstride ? rsrc(P + (size_t)tile * lp * FPHE_WAVE, lp * 256u) : rsrc(P, lp * 256u);
+    const bool nd = inside && need[elem] != 0;
+    const __amdgpu_buffer_rsrc_t Er = rsrc(Ex + (size_t)tile * L1 * FPHE_WAVE, L1 * 256u);
     const ColIO Ai = colio(Ca + (size_t)tile * L32 * FPHE_WAVE, L32, col, 32u * g.q);
+    const ColIO Ii = colio(Cinv + (size_t)tile * L32 * FPHE_WAVE, L32, col, 32u * g.q);
     const ColIO Oo = colio(Co + (size_t)tile * L32 * FPHE_WAVE, L32, col, 32u * g.q);
-    // classify the significand (:335-344); every lane of the element does the same scan
-    u32 any = 0;
-    int ebits = 0;
-    u32 br_max = 0, br_nmm = 0;
-#pragma unroll 4
-    for (u32 j = 0; j < L1; ++j) {
-      const u32 pj = j < lp ? tld(Pr, pcol, j) : 0u;
-      any |= pj;
-      if (pj) ebits = 32 * (int)j + 32 - __clz(pj);
-      const u64 d1 = (u64)K.max_int[j] - pj - br_max;
-      br_max = (u32)(d1 >> 63);
-      const u64 d2 = (u64)pj - K.n_mm[j] - br_nmm;
-      br_nmm = (u32)(d2 >> 63);
-    }
-    const bool isneg = (pneg[pe] != 0) && (any != 0);
-    const bool big = !isneg && (br_nmm == 0);
-    const bool invalid = !isneg && !big && (br_max != 0);
-    u32 ef = 0;
-    if (isneg || big) ef |= FPHE_EF_NOT_INVERTIBLE;
-    if (invalid) ef |= FPHE_EF_MUL_INVALID_PT;
-    if (g.q == 0 && elem < count) set_err(err, ef);
-    if (isneg || big || invalid) ebits = 0;
+    const int ebits = inside ? ebits_in[elem] : 0;
     const int maxbits = wave_max_int(ebits);
     L27 A;
-    load_chunk(A, 2u * g.q, [&](int k) { return Ai.ld(k); });
+    load_chunk(A, 2u * g.q, [&](int k) { return nd ? Ii.ld(k) : Ai.ld(k); });
     const_to_slot<TPI>(bcol, qoff, K.N2R2_27, g.q);
-    mont_mul<TPI>(A, bcol, N, np, g.q);  // X = c R
+    mont_mul<TPI>(A, bcol, N, np, g.q);  // X = base R
     if (maxbits > 0) {
       to_slot<TPI>(bcol, qoff, A);
       tab_store(tb, 1, A);
@@ -393,11 +432,12 @@ __global__ __launch_bounds__(kBlock) void k_mul27(KeyArgs K, const u32* __restri
       auto digit = [&](int wi) -> u32 {
         const int b0 = wi * W;
         const u32 limb = (u32)(b0 >> 5);
-        const u32 v = limb < lp ? tld(Pr, pcol, limb) : 0u;
-        const u32 dd = (v >> (b0 & 31)) & ((1u << W) - 1);
-        return ebits == 0 ? 0u : dd;
+        const int off = b0 & 31;
+        u32 v = tld(Er, col, limb) >> off;
+        if (off + W > 32 && limb + 1 < L1) v |= tld(Er, col, limb + 1) << (32 - off);
+        return ebits == 0 ? 0u : (v & ((1u << W) - 1));
       };
-      auto entry_tile = [&](u32 dgt) {  // per-lane entry through the lane-varying voffset
+      auto entry_tile = [&](u32 dgt) {  // per-element entry through the lane-varying voffset
         Tile t = tb;
         t.vo = tb.vo + dgt * LL * 256u;
         return t;
@@ -418,10 +458,169 @@ __global__ __launch_bounds__(kBlock) void k_mul27(KeyArgs K, const u32* __restri
     mont_mul<TPI>(A, bcol, N, np, g.q);  // leave Montgomery form (<= N)
     finalize<TPI>(A, N, g.q);
     store_chunk<TPI>(A, g.q, [&](int k, u32 v) { Oo.st(k, v); });
-    if (g.q == 0 && elem < count) {
+    if (g.q == 0 && inside) {
       so[elem] = 0;
       eo[elem] = ea[elem] + pexp[pe];
     }
+  }
+}
+
+// ======================================================================================
+// Co = Ca^(2^nsq) * Cb mod n^2, sign = sign(b): one step of pack_squeeze
+// (fixedpoint_paillier/src/lib.rs:439-450: result.pow_mod_mut(2^shift) then
+// result * y % ns; the powm result is canonical, so the product's sign is y's).
+// ======================================================================================
+template <int L>
+__global__ __launch_bounds__(kBlock) void k_sqmul27(KeyArgs K, const u32* __restrict__ Ca, const u32* __restrict__ Cb,
+                                                    const u8* __restrict__ sb, int nsq, size_t count,
+                                                    u32* __restrict__ Co, u8* __restrict__ so, u32 ldsw) {
+  constexpr int TPI = L / 32;
+  using G = Geo<TPI>;
+  constexpr int E = G::E;
+  constexpr u32 L32 = L;
+  extern __shared__ __attribute__((aligned(16))) u32 lds[];
+  G g;
+  const u32 wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u32 gw = blockIdx.x * kWavesPerBlock + wib, nw = gridDim.x * kWavesPerBlock;
+  u32* bcol = lds + wib * ldsw * E + g.e;
+  const u32 qoff = lds_qoff<TPI>(g.q);
+  Mod<TPI> N;
+  N.init(K.N2_27, g.q);
+  const u32 np = K.n2_np27;
+  const u32 nwt = (u32)((count + E - 1) / E);
+  for (u32 wt = gw; wt < nwt; wt += nw) {
+    const size_t ebase = (size_t)wt * E;
+    const u32 tile = (u32)(ebase >> 6);
+    const u32 col = (u32)(ebase & 63) + (u32)g.e;
+    const size_t elem = ebase + g.e;
+    const ColIO Ai = colio(Ca + (size_t)tile * L32 * FPHE_WAVE, L32, col, 32u * g.q);
+    const ColIO Bi = colio(Cb + (size_t)tile * L32 * FPHE_WAVE, L32, col, 32u * g.q);
+    const ColIO Oo = colio(Co + (size_t)tile * L32 * FPHE_WAVE, L32, col, 32u * g.q);
+    L27 A, B;
+    load_chunk(A, 2u * g.q, [&](int k) { return Ai.ld(k); });
+    const_to_slot<TPI>(bcol, qoff, K.N2R2_27, g.q);
+    mont_mul<TPI>(A, bcol, N, np, g.q);  // a R
+#pragma unroll 1
+    for (int k = 0; k < nsq; ++k) sqr<TPI>(A, bcol, qoff, N, np, g.q);
+    load_chunk(B, 2u * g.q, [&](int k) { return Bi.ld(k); });
+    to_slot<TPI>(bcol, qoff, B);
+    mont_mul<TPI>(A, bcol, N, np, g.q);  // a^(2^nsq) b  (< 2N)
+    finalize<TPI>(A, N, g.q);
+    store_chunk<TPI>(A, g.q, [&](int k, u32 v) { Oo.st(k, v); });
+    if (g.q == 0 && elem < count) so[elem] = sb[elem];
+  }
+}
+
+// ======================================================================================
+// modular inverse of ciphertexts (GMP mpz_invert in math/src/rug/mod.rs:30-35; used by
+// neg/sub/rsub, fixedpoint_paillier/src/lib.rs:259-285, and the invert branches of mul,
+// :334-349).  Step 1: x0 = c^-1 mod n (safegcd, inv27.h) into X0 [tile][L1][64];
+// step 2 (k_inv_lift27): c^-1 mod n^2 = x0 (2 - c x0).  need[e] == 0 skips an element
+// (a wave with no such element skips the tile); need == nullptr means every element.
+// ======================================================================================
+template <int L>
+__global__ __launch_bounds__(kBlock) void k_inv_n27(KeyArgs K, const u32* __restrict__ C, size_t count,
+                                                    const u8* __restrict__ need, u32* __restrict__ X0,
+                                                    int32_t* __restrict__ err, u32 ldsw) {
+  constexpr int TPI = L / 64;  // n: 76 limbs for 2048-bit keys, 38 for 1024-bit
+  using G = Geo<TPI>;
+  constexpr int E = G::E, NL = G::NL;
+  constexpr u32 L32 = L, L1 = L / 2;
+  constexpr int kBatches = (49 * (L1 * 32) + 80) / 17 / LB + 2;  // Bernstein-Yang bound / 27, + margin
+  extern __shared__ __attribute__((aligned(16))) u32 lds[];
+  G g;
+  const u32 wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u32 gw = blockIdx.x * kWavesPerBlock + wib, nw = gridDim.x * kWavesPerBlock;
+  u32* bcol = lds + wib * ldsw * E + g.e;
+  const u32 qoff = lds_qoff<TPI>(g.q);
+  Mod<TPI> N;
+  N.init(K.Nn_27, g.q);
+  const u32 np = K.nn_np27;
+  const u32 nwt = (u32)((count + E - 1) / E);
+  for (u32 wt = gw; wt < nwt; wt += nw) {
+    const size_t ebase = (size_t)wt * E;
+    const u32 tile = (u32)(ebase >> 6);
+    const u32 col = (u32)(ebase & 63) + (u32)g.e;
+    const size_t elem = ebase + g.e;
+    const bool nd = elem < count && (need == nullptr || need[elem] != 0);
+    if (!__any(nd)) continue;
+    const u32* ctile = C + (size_t)tile * L32 * FPHE_WAVE;
+    // x = c mod n: c = c_lo + R c_hi, R = 2^(27 NL); mont(c_lo, R mod n) + mont(c_hi, R^2 mod n)
+    L27 A, B;
+    {
+      const u32 bit0 = 27u * NL + 1026u * g.q;
+      const ColIO Ci = colio(ctile, L32, col, bit0 >> 5);
+      load_chunk(B, bit0 & 31u, [&](int k) { return Ci.ld(k); });
+    }
+    const_to_slot<TPI>(bcol, qoff, K.NnR2_27, g.q);
+    mont_mul<TPI>(B, bcol, N, np, g.q);
+    {
+      const ColIO Ci = colio(ctile, L32, col, 32u * g.q);
+      load_chunk(A, 2u * g.q, [&](int k) { return Ci.ld(k); });
+    }
+    const_to_slot<TPI>(bcol, qoff, K.NnR1_27, g.q);
+    mont_mul<TPI>(A, bcol, N, np, g.q);
+#pragma unroll
+    for (int j = 0; j < LL; ++j) A.set(j, A[j] + B[j]);
+    normalize_exact<TPI>(A, g.q);  // < 4n
+    finalize<TPI>(A, N, g.q);
+    finalize<TPI>(A, N, g.q);
+    finalize<TPI>(A, N, g.q);      // canonical c mod n
+    const bool ok = inv_mod<TPI>(A, N, K.nn_inv27, kBatches, g.q);
+    const ColIO Xo = colio(X0 + (size_t)tile * L1 * FPHE_WAVE, L1, col, 32u * g.q);
+    store_chunk<TPI>(A, g.q, [&](int k, u32 v) { Xo.st(k, v); });
+    if (g.q == 0 && nd && !ok) set_err(err, FPHE_EF_NOT_INVERTIBLE);
+  }
+}
+
+template <int L>
+__global__ __launch_bounds__(kBlock) void k_inv_lift27(KeyArgs K, const u32* __restrict__ C, size_t count,
+                                                       const u8* __restrict__ need, const u32* __restrict__ X0,
+                                                       u32* __restrict__ Co, u32 ldsw) {
+  constexpr int TPI = L / 32;
+  using G = Geo<TPI>;
+  constexpr int E = G::E;
+  constexpr u32 L32 = L, L1 = L / 2;
+  extern __shared__ __attribute__((aligned(16))) u32 lds[];
+  G g;
+  const u32 wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u32 gw = blockIdx.x * kWavesPerBlock + wib, nw = gridDim.x * kWavesPerBlock;
+  u32* bcol = lds + wib * ldsw * E + g.e;
+  const u32 qoff = lds_qoff<TPI>(g.q);
+  Mod<TPI> N;
+  N.init(K.N2_27, g.q);
+  const u32 np = K.n2_np27;
+  const u32 nwt = (u32)((count + E - 1) / E);
+  for (u32 wt = gw; wt < nwt; wt += nw) {
+    const size_t ebase = (size_t)wt * E;
+    const u32 tile = (u32)(ebase >> 6);
+    const u32 col = (u32)(ebase & 63) + (u32)g.e;
+    const size_t elem = ebase + g.e;
+    const bool nd = elem < count && (need == nullptr || need[elem] != 0);
+    if (!__any(nd)) continue;
+    L27 A;
+    {
+      const ColIO Xi = colio(X0 + (size_t)tile * L1 * FPHE_WAVE, L1, col, 32u * g.q);
+      load_chunk(A, 2u * g.q, [&](int k) { return Xi.ld(k); });
+    }
+    const_to_slot<TPI>(bcol, qoff, K.N2R2_27, g.q);
+    mont_mul<TPI>(A, bcol, N, np, g.q);  // x0 R
+    to_slot<TPI>(bcol, qoff, A);         // the slot keeps x0 R for the rest of the element
+    {
+      const ColIO Ci = colio(C + (size_t)tile * L32 * FPHE_WAVE, L32, col, 32u * g.q);
+      load_chunk(A, 2u * g.q, [&](int k) { return Ci.ld(k); });
+    }
+    mont_mul<TPI>(A, bcol, N, np, g.q);  // c x0 (plain form: c R^0 x0 R / R)
+    // s = 2 - c x0  as  (2 + 2N - t) with t < 2N: positive, < 4N
+    from_signed<TPI>(A, [&](int j) {
+      return (int64_t)((j == 0 && g.q == 0) ? 2 : 0) + 2 * (int64_t)N(j) - (int64_t)A[j];
+    }, g.q);
+    mont_mul<TPI>(A, bcol, N, np, g.q);  // x0 (2 - c x0) R / R = x  (< 2N)
+    finalize<TPI>(A, N, g.q);
+    const ColIO Oo = colio(Co + (size_t)tile * L32 * FPHE_WAVE, L32, col, 32u * g.q);
+    store_chunk<TPI>(A, g.q, [&](int k, u32 v) {
+      if (nd) Oo.st(k, v);
+    });
   }
 }
 

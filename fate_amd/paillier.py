@@ -256,6 +256,7 @@ class PlaintextVector:
         return [Plaintext(self._gather(torch.tensor([i], device=self.device))) for i in range(self.count)]
 
     def _gather(self, idx: torch.Tensor) -> "PlaintextVector":
+        idx = idx.to(self.device)
         cols = tiles_to_cols(self.P)[:, idx]
         return PlaintextVector(cols_to_tiles(cols), _pad_flat(self.neg[idx], len(idx)),
                                _pad_flat(self.exp[idx], len(idx)), len(idx))
@@ -433,6 +434,48 @@ class CiphertextVector:
         b = other.slice(sb, size)
         self._assign(torch.arange(sa, sa + size), _add(pk, a, b, broadcast=False))
 
+    def neg(self, pk: "PK") -> "CiphertextVector":
+        """Element-wise ``Ciphertext::neg`` (lib.rs:259-264): (invert(c, n^2), exp)."""
+        return _neg(pk, self)
+
+    def sub(self, pk: "PK", other: "CiphertextVector") -> "CiphertextVector":
+        """``CiphertextVector::sub`` (lib.rs:812-820): x.add(y.neg())."""
+        return _add(pk, self, _neg(pk, other), broadcast=False)
+
+    def sub_scalar(self, pk: "PK", other: "Ciphertext") -> "CiphertextVector":
+        """``CiphertextVector::sub_scalar`` (lib.rs:822-825)."""
+        return _add(pk, self, _neg(pk, other.vec), broadcast=True)
+
+    def rsub(self, pk: "PK", other: "CiphertextVector") -> "CiphertextVector":
+        """``CiphertextVector::rsub`` (lib.rs:827-835): y.sub(x) = y.add(x.neg())."""
+        n = min(self.count, other.count)
+        return _add(pk, other, _neg(pk, self, count=n), broadcast=False, count=n)
+
+    def rsub_scalar(self, pk: "PK", other: "Ciphertext") -> "CiphertextVector":
+        """``CiphertextVector::rsub_scalar`` (lib.rs:837-840): other.sub(x) = other.add(x.neg())."""
+        neg = _neg(pk, self)
+        return _add(pk, neg, other.vec, broadcast=True)
+
+    def isub(self, pk: "PK", other: "CiphertextVector") -> None:
+        """In-place sub (x.sub_assign(y) over zip, lib.rs:289-292)."""
+        r = self.sub(pk, other)
+        self._overwrite_prefix(r)
+
+    def isub_vec(self, other: "CiphertextVector", sa: int, sb: int, size: Optional[int], pk: "PK") -> None:
+        """``CiphertextVector::isub_vec`` (lib.rs:679-722)."""
+        if size is None:
+            size = min(self.count - sa, other.count - sb)
+        else:
+            if sa + size > self.count:
+                raise RuntimeError(f"end index out of range: sa={sa}, ea={sa + size}, data_size={self.count}")
+            if sb + size > other.count:
+                raise RuntimeError(f"end index out of range: sb={sb}, eb={sb + size}, data_size={other.count}")
+        if size <= 0:
+            return
+        a = self.slice(sa, size)
+        b = other.slice(sb, size)
+        self._assign(torch.arange(sa, sa + size), a.sub(pk, b))
+
     def mul(self, pk: "PK", other: PlaintextVector) -> "CiphertextVector":
         """``CiphertextVector::mul`` (lib.rs:842-850)."""
         return _mul(pk, self, other, broadcast=False)
@@ -440,6 +483,159 @@ class CiphertextVector:
     def mul_scalar(self, pk: "PK", other: Plaintext) -> "CiphertextVector":
         """``CiphertextVector::mul_scalar`` (lib.rs:852-859)."""
         return _mul(pk, self, other.vec, broadcast=True)
+
+    # ---- SecureBoost / Hetero-LR vector ops (fixedpoint_paillier/src/lib.rs:417-909) -----
+    # Folds and scans are trees of the device ct-add kernel.  Ciphertext addition is
+    # associative and commutative bit for bit (SURVEY.md §0 fact 3, tests/test_oracle.py),
+    # so a tree gives the reference's sequential result.
+    def iadd_slice(self, pk: "PK", position: int, other: Sequence["Ciphertext"]) -> None:
+        """``CiphertextVector::iadd_slice`` (lib.rs:509-513)."""
+        if not other:
+            return
+        o = Evaluator.cat([c.vec for c in other])
+        idx = torch.arange(position, position + o.count)
+        self._assign(idx, _add(pk, self._gather(idx), o, broadcast=False))
+
+    def iadd_vec_self(self, sa: int, sb: int, size: Optional[int], pk: "PK") -> None:
+        """``CiphertextVector::iadd_vec_self`` (lib.rs:521-568), including its in-place
+        cascade when the two ranges overlap (iadd_i_j, :417-424)."""
+        self._self_op(sa, sb, size, pk, sub=False)
+
+    def isub_vec_self(self, sa: int, sb: int, size: Optional[int], pk: "PK") -> None:
+        """``CiphertextVector::isub_vec_self`` (lib.rs:569-632)."""
+        self._self_op(sa, sb, size, pk, sub=True)
+
+    def _self_op(self, sa: int, sb: int, size: Optional[int], pk: "PK", sub: bool) -> None:
+        n = self.count
+        if sa == sb:
+            if size is not None and sa + size > n:
+                raise RuntimeError(f"end index out of range: sa={sa}, s={size}, data_size={n}")
+            end = n if size is None else sa + size
+            if end <= sa:
+                return
+            idx = torch.arange(sa, end)
+            if sub:  # x - x -> Ciphertext::zero() (lib.rs:578-588)
+                z = CiphertextVector.zeros(end - sa, self.L2, self.device)
+                self._assign(idx, z)
+            else:  # i_double: powm(c, 2) (lib.rs:294-299), = add(x, x)
+                x = self._gather(idx)
+                self._assign(idx, _add(pk, x, x, broadcast=False))
+            return
+        w0, r0 = max(sa, sb), min(sa, sb)
+        if size is not None and w0 + size > n:
+            nm = "sb" if sa < sb else "sa"
+            raise RuntimeError(f"end index out of range: {nm}={w0}, s={size}, data_size={n}")
+        s = (n - w0) if size is None else size
+        d = w0 - r0
+        # data[w0+k] op= data[r0+k] for k ascending; reads of r0+k >= w0 see earlier writes:
+        # process k in rounds of d so every round reads only finished values.
+        for start in range(0, s, d):
+            k = torch.arange(start, min(start + d, s))
+            x, y = self._gather(w0 + k), self._gather(r0 + k)
+            self._assign(w0 + k, x.sub(pk, y) if sub else _add(pk, x, y, broadcast=False))
+
+    def iupdate(self, other: "CiphertextVector", indexes, stride: int, pk: "PK") -> None:
+        """``CiphertextVector::iupdate`` (lib.rs:724-735): data[pos*stride+t] += other[i*stride+t]
+        for every position pos listed for sample i, folded per target slot on the device."""
+        ii, pp = _flatten_positions(indexes)
+        self._scatter_fold(other, ii, pp, stride, pk)
+
+    def iupdate_with_masks(self, other: "CiphertextVector", indexes, masks, stride: int, pk: "PK") -> None:
+        """``CiphertextVector::iupdate_with_masks`` (lib.rs:736-747): the k-th position list
+        belongs to the k-th sample whose mask is true."""
+        m = torch.as_tensor(list(masks) if not isinstance(masks, torch.Tensor) else masks, dtype=torch.bool)
+        vpos = torch.nonzero(m).squeeze(1)
+        ii, pp = _flatten_positions(indexes)
+        if ii.numel():
+            ii = vpos[ii]
+        self._scatter_fold(other, ii, pp, stride, pk)
+
+    def _scatter_fold(self, other: "CiphertextVector", ii: torch.Tensor, pp: torch.Tensor, stride: int,
+                      pk: "PK") -> None:
+        if ii.numel() == 0:
+            return
+        t = torch.arange(stride)
+        src = (ii[:, None] * stride + t).reshape(-1)
+        slot = (pp[:, None] * stride + t).reshape(-1)
+        if int(slot.max()) >= self.count or int(src.max()) >= other.count:
+            raise PanicException("index out of bounds")
+        uniq = torch.unique(slot)
+        terms = Evaluator.cat([self._gather(uniq), other._gather(src)])
+        folded, ids = _fold_segments(pk, terms, torch.cat([uniq, slot]))
+        self._assign(ids, folded)
+
+    def chunking_cumsum_with_step(self, pk: "PK", chunk_sizes: Sequence[int], step: int) -> None:
+        """``CiphertextVector::chunking_cumsum_with_step`` (lib.rs:760-771): within each chunk,
+        data[i+j] += data[i+j-step] for j ascending -- an inclusive scan with stride `step`,
+        run as a Hillis-Steele scan (log2(chunk/step) rounds of the ct-add kernel)."""
+        sizes = [int(c) for c in chunk_sizes]
+        total = sum(sizes)
+        if total == 0 or step <= 0:
+            return
+        if total > self.count:
+            raise PanicException(f"index out of bounds: the len is {self.count} but the index is {total - 1}")
+        starts = torch.repeat_interleave(torch.tensor([0] + list(itertools.accumulate(sizes))[:-1]),
+                                         torch.tensor(sizes))
+        rel = torch.arange(total) - starts
+        shift = step
+        while shift < max(sizes):
+            idx = torch.nonzero(rel >= shift).squeeze(1)
+            if idx.numel() == 0:
+                break
+            x, y = self._gather(idx), self._gather(idx - shift)
+            self._assign(idx, _add(pk, x, y, broadcast=False))
+            shift *= 2
+
+    def intervals_sum_with_step(self, pk: "PK", intervals: Sequence[Tuple[int, int]], step: int
+                                ) -> "CiphertextVector":
+        """``CiphertextVector::intervals_sum_with_step`` (lib.rs:773-788): out[i*step + c] =
+        fold of data[s+k] over k = c (mod step), s+k < e, from zero."""
+        out = CiphertextVector.zeros(len(intervals) * step, self.L2, self.device)
+        idx, seg = [], []
+        for i, (s_, e_) in enumerate(intervals):
+            if e_ > self.count or s_ > e_:
+                raise PanicException(f"range end index {e_} out of range for slice of length {self.count}")
+            k = torch.arange(s_, e_)
+            idx.append(k)
+            seg.append(i * step + (k - s_) % step)
+        if idx:
+            ia, sa_ = torch.cat(idx), torch.cat(seg)
+            if ia.numel():
+                folded, ids = _fold_segments(pk, self._gather(ia), sa_)
+                out._assign(ids, folded)
+        return out
+
+    def pack_squeeze(self, pack_num: int, offset_bit: int, pk: "PK") -> "CiphertextVector":
+        """``CiphertextVector::pack_squeeze`` (paillier.rs:241; lib.rs:439-450): per chunk of
+        pack_num, acc = x0; acc = acc^(2^offset_bit) * y mod n^2 for each further y; exp 0."""
+        n = self.count
+        heads = torch.arange(0, n, pack_num)
+        acc = self._gather(heads)
+        for j in range(1, pack_num):
+            ch = torch.nonzero(heads + j < n).squeeze(1)
+            if ch.numel() == 0:
+                break
+            y = self._gather(heads[ch] + j)
+            acc._assign(ch, _sqmul(pk, acc._gather(ch), y, offset_bit))
+        acc.exp.zero_()
+        return acc
+
+    def matmul(self, pk: "PK", other: PlaintextVector, lshape, rshape) -> "CiphertextVector":
+        """``CiphertextVector::matmul`` (lib.rs:861-880): out[i,j] = sum_k self[i,k] * other[k,j]."""
+        I, K = int(lshape[0]), int(lshape[1])
+        J = int(rshape[1])
+        i, j, k = torch.meshgrid(torch.arange(I), torch.arange(J), torch.arange(K), indexing="ij")
+        return _matmul_terms(pk, self, other, (i * K + k).reshape(-1), (k * J + j).reshape(-1),
+                             (i * J + j).reshape(-1), I * J)
+
+    def rmatmul(self, pk: "PK", other: PlaintextVector, lshape, rshape) -> "CiphertextVector":
+        """``CiphertextVector::rmatmul`` (lib.rs:882-908): out[i,j] = sum_k other[i,k] * self[k,j]
+        with self (lshape) = [K, Jl], other (rshape) = [I, K]."""
+        Jl = int(lshape[1])
+        I, K = int(rshape[0]), int(rshape[1])
+        i, j, k = torch.meshgrid(torch.arange(I), torch.arange(Jl), torch.arange(K), indexing="ij")
+        return _matmul_terms(pk, self, other, (k * Jl + j).reshape(-1), (i * K + k).reshape(-1),
+                             (i * Jl + j).reshape(-1), I * Jl)
 
     def _overwrite_prefix(self, r: "CiphertextVector") -> None:
         if r.count == self.count:
@@ -478,6 +674,101 @@ def _add(pk: "PK", a: CiphertextVector, b: CiphertextVector, broadcast: bool, co
     return out
 
 
+def _flatten_positions(indexes) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Vec<Vec<usize>> of positions per sample -> (sample ids, positions), flat."""
+    if isinstance(indexes, torch.Tensor):
+        if indexes.dim() != 2:
+            raise ValueError("positions tensor must be 2-D [samples, positions]")
+        ns, npos = indexes.shape
+        return torch.arange(ns).repeat_interleave(npos), indexes.reshape(-1).long().cpu()
+    lens = [len(x) for x in indexes]
+    if sum(lens) == 0:
+        return torch.zeros(0, dtype=torch.long), torch.zeros(0, dtype=torch.long)
+    ii = torch.arange(len(lens)).repeat_interleave(torch.tensor(lens))
+    pp = torch.tensor(list(itertools.chain.from_iterable(indexes)), dtype=torch.long)
+    return ii, pp
+
+
+def _fold_segments(pk: "PK", src: CiphertextVector, seg: torch.Tensor) -> Tuple[CiphertextVector, torch.Tensor]:
+    """Fold src by segment id with the ct-add kernel, as a pairwise tree inside each
+    segment (ceil(log2(longest segment)) launches).  Returns one folded ciphertext per
+    non-empty segment, with the segment ids (ascending)."""
+    dev = src.device
+    seg = seg.to(dev, torch.long)
+    order = torch.argsort(seg, stable=True)
+    ids = seg[order]
+    cur = src._gather(order)
+    while ids.numel() > 1:
+        n = ids.numel()
+        pos = torch.arange(n, device=dev)
+        head = torch.ones(n, dtype=torch.bool, device=dev)
+        head[1:] = ids[1:] != ids[:-1]
+        start = torch.cummax(torch.where(head, pos, torch.zeros_like(pos)), 0).values
+        left = pos[(pos - start) % 2 == 0]
+        nxt = torch.clamp(left + 1, max=n - 1)
+        has = (left + 1 < n) & (ids[nxt] == ids[left])
+        if not bool(has.any()):
+            break
+        pl = left[has]
+        summed = _add(pk, cur._gather(pl), cur._gather(pl + 1), broadcast=False)
+        new = cur._gather(left)
+        new._assign(torch.nonzero(has).squeeze(1), summed)
+        cur, ids = new, ids[left]
+    return cur, ids
+
+
+def _matmul_terms(pk: "PK", a: CiphertextVector, b: PlaintextVector, ai: torch.Tensor, bi: torch.Tensor,
+                  oi: torch.Tensor, nout: int, chunk: int = 1 << 22) -> CiphertextVector:
+    """out[o] = fold over terms t with oi[t] == o of a[ai[t]] * b[bi[t]], from zero; the
+    products run through the ct x pt kernel, the folds through the ct-add kernel, in chunks
+    of `chunk` terms so the materialised products stay bounded."""
+    out = CiphertextVector.zeros(nout, a.L2, a.device)
+    for s0 in range(0, ai.numel(), chunk):
+        sl = slice(s0, s0 + chunk)
+        prod = _mul(pk, a._gather(ai[sl]), b._gather(bi[sl].to(b.device)), broadcast=False)
+        seg = oi[sl]
+        if s0:  # fold the running partial sums in with this chunk's terms
+            touched = torch.unique(seg)
+            prod = Evaluator.cat([out._gather(touched), prod])
+            seg = torch.cat([touched, seg])
+        folded, ids = _fold_segments(pk, prod, seg)
+        out._assign(ids, folded)
+    return out
+
+
+def _sqmul(pk: "PK", a: CiphertextVector, b: CiphertextVector, nsq: int) -> CiphertextVector:
+    """(a^(2^nsq) * b mod n^2, sign of b) on the device (fphe_sqmul)."""
+    dev = a.device
+    a, b = _fit_limbs(a, pk._key.L2), _fit_limbs(b, pk._key.L2)
+    n = min(a.count, b.count)
+    out = CiphertextVector.empty(n, a.L2, dev)
+    if n == 0:
+        return out
+    lib = _lib.load()
+    ctx = pk._key.ctx(dev)
+    _lib.check(lib.fphe_sqmul(ctx, _ptr(a.C), _ptr(b.C), _ptr(b.sign), int(nsq), n, _ptr(out.C), _ptr(out.sign),
+                              ctypes.c_void_p(_stream(dev))), "fphe_sqmul")
+    return out
+
+
+def _neg(pk: "PK", a: CiphertextVector, count: Optional[int] = None) -> CiphertextVector:
+    """(invert(C, n^2), sign 0, exp) on the device (fphe_neg)."""
+    dev = a.device
+    a = _fit_limbs(a, pk._key.L2)
+    n = a.count if count is None else count
+    out = CiphertextVector.empty(n, a.L2, dev)
+    if n == 0:
+        return out
+    lib = _lib.load()
+    ctx = pk._key.ctx(dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    _lib.check(lib.fphe_neg(ctx, _ptr(a.C), n, _ptr(out.C), _ptr(err), ctypes.c_void_p(_stream(dev))), "fphe_neg")
+    out.exp[:n] = a.exp[:n]
+    if int(err.item()) & _lib.EF_NOT_INVERTIBLE:
+        raise PanicException("called `Option::unwrap()` on a `None` value")  # invert().unwrap() (math/src/rug/mod.rs:30-35)
+    return out
+
+
 def _mul(pk: "PK", a: CiphertextVector, p: PlaintextVector, broadcast: bool) -> CiphertextVector:
     dev = a.device
     a = _fit_limbs(a, pk._key.L2)
@@ -496,7 +787,7 @@ def _mul(pk: "PK", a: CiphertextVector, p: PlaintextVector, broadcast: bool) -> 
     if v & _lib.EF_MUL_INVALID_PT:
         raise PanicException("invalid plaintext")
     if v & _lib.EF_NOT_INVERTIBLE:
-        raise NotImplementedError("ct x negative plaintext needs a modular inverse: not yet implemented on device")
+        raise PanicException("called `Option::unwrap()` on a `None` value")  # invert().unwrap() (math/src/rug/mod.rs:30-35)
     return out
 
 

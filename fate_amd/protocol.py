@@ -178,6 +178,42 @@ class evaluator:
         return a.add_scalar(pk.pk, encrypted)
 
     @staticmethod
+    def sub(a: EV, b: EV, pk: PK):
+        return a.sub(pk.pk, b)
+
+    @staticmethod
+    def sub_plain(a: EV, b: V, pk: PK, coder: Coder, output_dtype=None):
+        if output_dtype is None:
+            output_dtype = b.dtype
+        encoded = coder.encode_tensor(b, dtype=output_dtype)
+        encrypted = pk.encrypt_encoded(encoded, obfuscate=False)
+        return a.sub(pk.pk, encrypted)
+
+    @staticmethod
+    def sub_plain_scalar(a: EV, b, pk: PK, coder: Coder, output_dtype):
+        encoded = coder.encode(b, dtype=output_dtype)
+        encrypted = pk.encrypt_encoded_scalar(encoded, obfuscate=False)
+        return a.sub_scalar(pk.pk, encrypted)
+
+    @staticmethod
+    def rsub(a: EV, b: EV, pk: PK):
+        return a.rsub(pk.pk, b)
+
+    @staticmethod
+    def rsub_plain(a: EV, b: V, pk: PK, coder: Coder, output_dtype=None):
+        if output_dtype is None:
+            output_dtype = b.dtype
+        encoded = coder.encode_tensor(b, dtype=output_dtype)
+        encrypted = pk.encrypt_encoded(encoded, obfuscate=False)
+        return a.rsub(pk.pk, encrypted)
+
+    @staticmethod
+    def rsub_plain_scalar(a: EV, b, pk: PK, coder: Coder, output_dtype):
+        encoded = coder.encode(b, dtype=output_dtype)
+        encrypted = pk.encrypt_encoded_scalar(encoded, obfuscate=False)
+        return a.rsub_scalar(pk.pk, encrypted)
+
+    @staticmethod
     def mul_plain(a: EV, b: V, pk: PK, coder: Coder, output_dtype=None):
         if output_dtype is None:
             output_dtype = b.dtype
@@ -190,14 +226,52 @@ class evaluator:
         return a.mul_scalar(pk.pk, encoded)
 
     @staticmethod
+    def matmul(a: EV, b: V, a_shape, b_shape, pk: PK, coder: Coder, output_dtype):
+        encoded = coder.encode_tensor(b, dtype=output_dtype)
+        return a.matmul(pk.pk, encoded, a_shape, b_shape)
+
+    @staticmethod
+    def rmatmul(a: EV, b: V, a_shape, b_shape, pk: PK, coder: Coder, output_dtype):
+        encoded = coder.encode_tensor(b, dtype=output_dtype)
+        return a.rmatmul(pk.pk, encoded, a_shape, b_shape)
+
+    @staticmethod
     def zeros(size, dtype) -> EV:
         return CiphertextVector.zeros(size)
 
     @staticmethod
     def i_add(pk: PK, a: EV, b: EV, sa=0, sb=0, size: Optional[int] = None) -> None:
         if a is b:
-            raise NotImplementedError("iadd_vec_self: not yet implemented on device")
-        a.iadd_vec(b, sa, sb, size, pk.pk)
+            a.iadd_vec_self(sa, sb, size, pk.pk)
+        else:
+            a.iadd_vec(b, sa, sb, size, pk.pk)
+
+    @staticmethod
+    def i_sub(pk: PK, a: EV, b: EV, sa=0, sb=0, size: Optional[int] = None) -> None:
+        if a is b:
+            a.isub_vec_self(sa, sb, size, pk.pk)
+        else:
+            a.isub_vec(b, sa, sb, size, pk.pk)
+
+    @staticmethod
+    def i_update(pk: PK, a: EV, b: EV, positions, stride: int) -> None:
+        a.iupdate(b, positions, stride, pk.pk)
+
+    @staticmethod
+    def i_update_with_masks(pk: PK, a: EV, b: EV, positions, masks, stride: int) -> None:
+        a.iupdate_with_masks(b, positions, masks, stride, pk.pk)
+
+    @staticmethod
+    def chunking_cumsum_with_step(pk: PK, a: EV, chunk_sizes: List[int], step: int):
+        return a.chunking_cumsum_with_step(pk.pk, chunk_sizes, step)
+
+    @staticmethod
+    def intervals_sum_with_step(pk: PK, a: EV, intervals: List[Tuple[int, int]], step: int):
+        return a.intervals_sum_with_step(pk.pk, intervals, step)
+
+    @staticmethod
+    def pack_squeeze(a: EV, pack_num: int, shift_bit: int, pk: PK) -> EV:
+        return a.pack_squeeze(pack_num, shift_bit, pk.pk)
 
     @staticmethod
     def slice(a: EV, start: int, size: int) -> EV:

@@ -9,16 +9,20 @@
  *
  * Conventions
  *  - All vector buffers are DEVICE pointers (hipMalloc'd or torch CUDA tensors),
- *    laid out limb-major ("SoA"): limb j of element e lives at buf[j * count + e].
- *    Limbs are little-endian uint32 words.
+ *    laid out tile-major: a vector of `count` elements of W uint32 words each is
+ *    uint32 [T][W][64] with T = ceil(count/64); word j of element e lives at
+ *    buf[((e/64)*W + j)*64 + e%64].  Words are little-endian (word 0 least
+ *    significant).  Every 64-element tile is contiguous, so a wave reads word j of
+ *    its 64 elements as one 256-byte row.  Per-element byte/int arrays (sign, neg,
+ *    exp) are flat [T*64].  Buffers are padded to whole tiles.
  *  - A ciphertext vector is (C, sign, exp):
- *      C    : uint32 [L2][count]   canonical residue in [0, n^2), L2 = key_bits/16
- *      sign : uint8  [count]       1 iff the reference's signed integer is C - n^2
- *      exp  : int32  [count]       base-16 fixed-point exponent
+ *      C    : uint32 [T][L2][64]   canonical residue in [0, n^2), L2 = key_bits/16
+ *      sign : uint8  [T*64]        1 iff the reference's signed integer is C - n^2
+ *      exp  : int32  [T*64]        base-16 fixed-point exponent
  *    The reference keeps ciphertexts as signed rug::Integer values because rug's
  *    `%` truncates; (C, sign) is that integer, losslessly.
- *  - A plaintext vector is (P, neg, exp): magnitude limbs uint32 [lp][count],
- *    neg uint8 [count] (1 = negative significand), exp int32 [count].
+ *  - A plaintext vector is (P, neg, exp): magnitude words uint32 [T][lp][64],
+ *    neg uint8 [T*64] (1 = negative significand), exp int32 [T*64].
  *  - `stream` is a hipStream_t (NULL = default stream).  Calls are asynchronous
  *    on that stream; per-element error flags land in a device int32 word that the
  *    caller reads after synchronising.
@@ -65,7 +69,7 @@ fphe_status fphe_ctx_limbs(const fphe_ctx* ctx, uint32_t* l2, uint32_t* l1);
 
 /* Device-side fixed-point encode of float32 (Coder.encode_f32_vec, paillier.rs:162-169;
  * Coder::encode_f64, fixedpoint_paillier/src/lib.rs:148-168, 187-189).
- * Writes significand magnitude as 2 limbs P[2][count], neg[count], exp[count]. */
+ * Writes significand magnitude as 2 words P[T][2][64], neg, exp. */
 fphe_status fphe_encode_f32(const fphe_ctx* ctx, const float* x, size_t count,
                             uint32_t* P, uint8_t* neg, int32_t* exp, int32_t* err, void* stream);
 /* Same for float64 (Coder.encode_f64_vec, paillier.rs:145-152). */
@@ -73,7 +77,7 @@ fphe_status fphe_encode_f64(const fphe_ctx* ctx, const double* x, size_t count,
                             uint32_t* P, uint8_t* neg, int32_t* exp, int32_t* err, void* stream);
 
 /* Device-side decode (Coder.decode_f32_vec / decode_f64_vec, paillier.rs:153-161, 173-181;
- * Coder::decode_f64, fixedpoint_paillier/src/lib.rs:169-192).  P is [lp][count],
+ * Coder::decode_f64, fixedpoint_paillier/src/lib.rs:169-192).  P is [T][lp][64],
  * a non-negative decrypted significand (neg ignored: decrypt output is in [0,n)). */
 fphe_status fphe_decode_f32(const fphe_ctx* ctx, const uint32_t* P, uint32_t lp, const int32_t* exp,
                             size_t count, float* out, int32_t* err, void* stream);
@@ -83,13 +87,13 @@ fphe_status fphe_decode_f64(const fphe_ctx* ctx, const uint32_t* P, uint32_t lp,
 /* Encrypt encoded plaintexts: PK.encrypt_encoded (paillier.rs:51-57) ->
  * fixedpoint_paillier::PK::encrypt_encoded (lib.rs:370-381) -> paillier::PK::encrypt
  * (crates/paillier/src/lib.rs:104-121).
- *   P/neg      : plaintext significands, magnitude limbs [lp][count] (lp <= L1).
+ *   P/neg      : plaintext significands, magnitude words [T][lp][64] (lp <= L1).
  *   obfuscate  : 0 -> nude ciphertext 1+m*n (deterministic); 1 -> times r^n mod n^2.
  *   r          : NULL -> r drawn on the device from ChaCha20 keyed by rng_key[8]
  *                (uniform in [1, n-1] by rejection, as random.rs:22-25);
- *                else injected r, uint32 [L1][count] (parity/test mode).
+ *                else injected r, uint32 [T][L1][64] (parity/test mode).
  *   rng_nonce  : distinct per call with the same rng_key.
- * Outputs C[L2][count], sign[count].  (exp is copied by the caller.) */
+ * Outputs C[T][L2][64], sign.  (exp is copied by the caller.) */
 fphe_status fphe_encrypt(fphe_ctx* ctx, const uint32_t* P, uint32_t lp, const uint8_t* neg,
                          size_t count, int obfuscate, const uint32_t* r,
                          const uint32_t rng_key[8], uint64_t rng_nonce,
@@ -97,7 +101,7 @@ fphe_status fphe_encrypt(fphe_ctx* ctx, const uint32_t* P, uint32_t lp, const ui
 
 /* Decrypt to encoded plaintext: SK.decrypt_to_encoded (paillier.rs:79-81) ->
  * paillier::SK::decrypt (crates/paillier/src/lib.rs:163-176), CRT.
- * Output P[L1][count] in [0, n). */
+ * Output P[T][L1][64] in [0, n). */
 fphe_status fphe_decrypt(fphe_ctx* ctx, const uint32_t* C, size_t count, uint32_t* P, void* stream);
 
 /* Ciphertext add with exponent alignment and the literal-1 rule:
@@ -109,11 +113,25 @@ fphe_status fphe_add(fphe_ctx* ctx,
                      size_t count, uint32_t* Co, uint8_t* so, int32_t* eo, void* stream);
 
 /* Ciphertext x plaintext: CiphertextVector.mul (paillier.rs:361) -> Ciphertext::mul
- * (fixedpoint_paillier/src/lib.rs:334-349).  Plaintext (P[lp][count], neg, pexp);
+ * (fixedpoint_paillier/src/lib.rs:334-349).  Plaintext (P[T][lp][64], neg, pexp);
  * p_stride = 0 broadcasts element 0 (mul_scalar, paillier.rs:364). */
 fphe_status fphe_mul(fphe_ctx* ctx, const uint32_t* Ca, const uint8_t* sa, const int32_t* ea,
                      const uint32_t* P, uint32_t lp, const uint8_t* pneg, const int32_t* pexp, int p_stride,
                      size_t count, uint32_t* Co, uint8_t* so, int32_t* eo, int32_t* err, void* stream);
+
+/* Ciphertext inverse: Co = C^-1 mod n^2 (canonical; the caller sets sign 0 and copies
+ * exp).  This is the `neg` of Ciphertext::neg (fixedpoint_paillier/src/lib.rs:259-262,
+ * invert via math/src/rug/mod.rs:30-35), the building block of sub / rsub
+ * (CiphertextVector.sub/rsub, paillier.rs:349-358) and i_sub.  A non-unit C (the
+ * reference panics in invert().unwrap()) gives Co = 0 and FPHE_EF_NOT_INVERTIBLE. */
+fphe_status fphe_neg(fphe_ctx* ctx, const uint32_t* C, size_t count, uint32_t* Co, int32_t* err,
+                     void* stream);
+
+/* Co = Ca^(2^nsq) * Cb mod n^2 with so = sb: the step of CiphertextVector::pack_squeeze
+ * (paillier.rs:241-243; fixedpoint_paillier/src/lib.rs:439-450), `result.pow_mod_mut(2^shift)`
+ * then `result * y % ns` (the powm result is canonical, so the product takes y's sign). */
+fphe_status fphe_sqmul(fphe_ctx* ctx, const uint32_t* Ca, const uint32_t* Cb, const uint8_t* sb, uint32_t nsq,
+                       size_t count, uint32_t* Co, uint8_t* so, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,196 @@
+"""GPU parity of the vector algebra beyond encrypt/decrypt/add/mul: the modular inverse
+(neg, sub, rsub, the invert branches of ct x pt) and the SecureBoost / Hetero-LR vector
+ops (iupdate, chunking_cumsum_with_step, intervals_sum_with_step, pack_squeeze, matmul,
+rmatmul, iadd/isub_vec_self).  Expected values come from the CPU oracle
+(oracle/paillier_oracle.py, pinned against libgmp in tests/test_oracle.py) evaluated on
+the same inputs; comparison is bit-exact on signed ciphertext integers and exponents."""
+import json
+import os
+import random
+
+import pytest
+import torch
+
+from fate_amd import paillier as P
+from oracle import paillier_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def load(bits):
+    with open(os.path.join(HERE, "golden", f"paillier_{bits}.json")) as f:
+        fx = json.load(f)
+    p, q = int(fx["p"], 16), int(fx["q"], 16)
+    sk, pk, coder = P.keypair_from_primes(p, q)
+    osk, opk = O.keypair_from_primes(p, q)
+    cts = [O.Ciphertext(int(c, 16), e) for c, e in zip(fx["encrypt"]["ct"], fx["encrypt"]["exp"])]
+    return fx, sk, pk, coder, opk, cts
+
+
+@pytest.fixture(params=[1024, 2048], scope="module")
+def env(request):
+    return load(request.param)
+
+
+@pytest.fixture(scope="module")
+def env1024():
+    return load(1024)
+
+
+def dev_vec(pk, cts):
+    return P.CiphertextVector.from_signed_ints([c.c for c in cts], [c.exp for c in cts], pk.ns, pk._key.L2)
+
+
+def host(pk, v):
+    cs, es = v.to_signed_ints(pk.ns)
+    return list(zip(cs, es))
+
+
+def ref(cts):
+    return [(c.c, c.exp) for c in cts]
+
+
+def test_neg(env):
+    fx, sk, pk, coder, opk, cts = env
+    cts = cts + [O.ct_zero()]  # inv(1) = 1
+    out = dev_vec(pk, cts).neg(pk)
+    assert host(pk, out) == ref([O.ct_neg(opk, c) for c in cts])
+
+
+def test_sub_rsub(env):
+    fx, sk, pk, coder, opk, cts = env
+    a, b = cts[:40], cts[40:80]
+    va, vb = dev_vec(pk, a), dev_vec(pk, b)
+    assert host(pk, va.sub(pk, vb)) == ref(O.vec_sub(opk, a, b))
+    assert host(pk, va.rsub(pk, vb)) == ref(O.vec_rsub(opk, a, b))
+    s = P.Ciphertext(dev_vec(pk, [b[3]]))
+    assert host(pk, va.sub_scalar(pk, s)) == ref([O.ct_sub(opk, x, b[3]) for x in a])
+    assert host(pk, va.rsub_scalar(pk, s)) == ref([O.ct_sub(opk, b[3], x) for x in a])
+
+
+def test_decrypt_of_sub(env):
+    """dec(enc(x) - enc(y)) == x - y (reference round-trip style, crates/paillier/src/lib.rs:190-197)."""
+    fx, sk, pk, coder, opk, cts = env
+    x = torch.tensor(fx["encrypt"]["x_f32"][:48], dtype=torch.float64)
+    y = torch.tensor(fx["encrypt"]["x_f32"][48:96], dtype=torch.float64)
+    ex = pk.encrypt_encoded(coder.encode_f64_vec(x.cuda()), True)
+    ey = pk.encrypt_encoded(coder.encode_f64_vec(y.cuda()), True)
+    d = coder.decode_f64_vec(sk.decrypt_to_encoded(ex.sub(pk, ey))).cpu()
+    assert torch.allclose(d, x - y, rtol=0, atol=1e-9 * float((x.abs() + y.abs()).max()))
+
+
+def test_mul_negative_and_big_plaintexts(env):
+    fx, sk, pk, coder, opk, cts = env
+    rng = random.Random(5)
+    c = cts[:32]
+    sigs, exps = [], []
+    for i in range(32):
+        k = i % 4
+        if k == 0:
+            sigs.append(-rng.randrange(1, 1 << 53))          # negative float significand
+        elif k == 1:
+            sigs.append(opk.n - rng.randrange(1, 1 << 40))   # encoded negative int ("big")
+        elif k == 2:
+            sigs.append(rng.randrange(0, 1 << 56))           # ordinary
+        else:
+            sigs.append(-1)
+        exps.append(rng.randrange(-20, 3))
+    pv = P.PlaintextVector.from_ints(sigs, exps)
+    want = [O.ct_mul(opk, x, O.Plaintext(s, e)) for x, s, e in zip(c, sigs, exps)]
+    assert host(pk, dev_vec(pk, c).mul(pk, pv)) == ref(want)
+
+
+def test_mul_invalid_plaintext_panics(env1024):
+    fx, sk, pk, coder, opk, cts = env1024
+    pv = P.PlaintextVector.from_ints([opk.max_int + 1], [0])  # between max_int and n - max_int
+    with pytest.raises(P.PanicException):
+        dev_vec(pk, cts[:1]).mul(pk, pv)
+
+
+def test_pack_squeeze(env1024):
+    fx, sk, pk, coder, opk, cts = env1024
+    data = cts[:23]  # ragged last chunk
+    for pack_num, shift in ((2, 77), (3, 20), (1, 5)):
+        got = dev_vec(pk, data).pack_squeeze(pack_num, shift, pk)
+        assert host(pk, got) == ref(O.pack_squeeze(opk, data, pack_num, shift))
+
+
+def test_iupdate_and_masks(env1024):
+    fx, sk, pk, coder, opk, cts = env1024
+    rng = random.Random(7)
+    stride = 2
+    data = [O.ct_zero() for _ in range(10 * stride)]
+    data[3] = cts[90]  # a non-zero slot that also receives contributions
+    other = cts[:20 * stride]
+    indexes = [[rng.randrange(10) for _ in range(rng.randrange(0, 4))] for _ in range(20)]
+    v = dev_vec(pk, data)
+    v.iupdate(dev_vec(pk, other), indexes, stride, pk)
+    want = list(data)
+    O.iupdate(opk, want, other, indexes, stride)
+    assert host(pk, v) == ref(want)
+    masks = [rng.random() < 0.5 for _ in range(20)]
+    idx2 = [[rng.randrange(10)] for _ in range(sum(masks))]
+    v2 = dev_vec(pk, data)
+    v2.iupdate_with_masks(dev_vec(pk, other), idx2, masks, stride, pk)
+    want2 = list(data)
+    O.iupdate_with_masks(opk, want2, other, idx2, masks, stride)
+    assert host(pk, v2) == ref(want2)
+
+
+def test_chunking_cumsum_with_step(env1024):
+    fx, sk, pk, coder, opk, cts = env1024
+    data = cts[:24]
+    for sizes, step in (([4, 2, 6], 2), ([12, 12], 1), ([24], 3)):
+        v = dev_vec(pk, data)
+        v.chunking_cumsum_with_step(pk, sizes, step)
+        want = list(data)
+        O.chunking_cumsum_with_step(opk, want, sizes, step)
+        assert host(pk, v) == ref(want)
+
+
+def test_intervals_sum_with_step(env1024):
+    fx, sk, pk, coder, opk, cts = env1024
+    data = cts[:30]
+    intervals, step = [(0, 7), (7, 7), (10, 30)], 3
+    got = dev_vec(pk, data).intervals_sum_with_step(pk, intervals, step)
+    assert host(pk, got) == ref(O.intervals_sum_with_step(opk, data, intervals, step))
+
+
+def test_matmul_rmatmul(env1024):
+    fx, sk, pk, coder, opk, cts = env1024
+    rng = random.Random(3)
+    # a: 3x4 ciphertexts; b: 4x2 plaintexts with negative entries (invert branch)
+    a = cts[:12]
+    bs = [O.encode_f64(opk.n, rng.uniform(-3, 3)) for _ in range(8)]
+    pv = P.PlaintextVector.from_ints([b.significant for b in bs], [b.exp for b in bs])
+    got = dev_vec(pk, a).matmul(pk, pv, [3, 4], [4, 2])
+    assert host(pk, got) == ref(O.matmul(opk, a, bs, [3, 4], [4, 2]))
+    # rmatmul: self (lshape) 4x3 ciphertexts, other (rshape) 2x4 plaintexts
+    got = dev_vec(pk, a).rmatmul(pk, pv, [4, 3], [2, 4])
+    assert host(pk, got) == ref(O.rmatmul(opk, a, bs, [4, 3], [2, 4]))
+
+
+def _self_op_ref(opk, data, sa, sb, size, sub):
+    data = list(data)
+    if sa == sb:
+        end = len(data) if size is None else sa + size
+        for k in range(sa, end):
+            data[k] = O.ct_zero() if sub else O.ct_i_double(opk, data[k])
+        return data
+    w0, r0 = max(sa, sb), min(sa, sb)
+    s = len(data) - w0 if size is None else size
+    for k in range(s):  # iadd_i_j / isub_i_j (lib.rs:417-433)
+        data[w0 + k] = (O.ct_sub if sub else O.ct_add)(opk, data[w0 + k], data[r0 + k])
+    return data
+
+
+def test_iadd_isub_vec_self(env1024):
+    fx, sk, pk, coder, opk, cts = env1024
+    data = cts[:20]
+    for sa, sb, size in ((0, 3, 10), (5, 1, None), (4, 4, 6), (0, 10, 10)):
+        for sub in (False, True):
+            v = dev_vec(pk, data)
+            (v.isub_vec_self if sub else v.iadd_vec_self)(sa, sb, size, pk)
+            assert host(pk, v) == ref(_self_op_ref(opk, data, sa, sb, size, sub)), (sa, sb, size, sub)

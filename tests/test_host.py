@@ -73,9 +73,23 @@ def test_protocol_surface_matches_reference():
     from fate_amd import protocol
     for name in ("keygen", "evaluator", "SK", "PK", "Coder"):
         assert hasattr(protocol, name)
-    for m in ("add", "add_plain", "add_plain_scalar", "mul_plain", "mul_plain_scalar", "zeros", "i_add",
-              "slice", "i_shuffle", "shuffle", "intervals_slice", "cat"):
-        assert callable(getattr(protocol.evaluator, m))
+    # the TensorEvaluator static methods of protocol/phe/paillier.py:179-399
+    for m in ("add", "add_plain", "add_plain_scalar", "sub", "sub_plain", "sub_plain_scalar", "rsub",
+              "rsub_plain", "rsub_plain_scalar", "mul_plain", "mul_plain_scalar", "matmul", "rmatmul", "zeros",
+              "i_add", "i_sub", "slice", "i_shuffle", "shuffle", "i_update", "i_update_with_masks",
+              "intervals_slice", "cat", "chunking_cumsum_with_step", "pack_squeeze"):
+        assert callable(getattr(protocol.evaluator, m)), m
     for m in ("encode_tensor", "decode_tensor", "encode_vec", "decode_vec", "encode", "encode_f32_vec",
               "decode_f32_vec", "encode_i64_vec", "decode_i64_vec"):
         assert callable(getattr(protocol.Coder, m))
+
+
+def test_ciphertext_vector_surface_matches_reference():
+    """fate_amd.paillier.CiphertextVector has the pyo3 methods of paillier.rs:213-387."""
+    from fate_amd.paillier import CiphertextVector
+    for m in ("zeros", "pack_squeeze", "slice", "slice_indexes", "cat", "i_shuffle", "shuffle", "intervals_slice",
+              "iadd_slice", "iadd_vec_self", "isub_vec_self", "iadd_vec", "isub_vec", "iupdate",
+              "iupdate_with_masks", "iadd", "idouble", "chunking_cumsum_with_step", "intervals_sum_with_step",
+              "tolist", "add", "add_scalar", "sub", "sub_scalar", "rsub", "rsub_scalar", "mul", "mul_scalar",
+              "matmul", "rmatmul", "__len__"):
+        assert callable(getattr(CiphertextVector, m)), m
