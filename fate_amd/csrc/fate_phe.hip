@@ -24,7 +24,8 @@ namespace {
 
 constexpr int kBlock = 256;      // 4 waves per workgroup
 constexpr int kWavesPerBlock = kBlock / FPHE_WAVE;
-constexpr int kWinEnc = 5;       // window of the shared-exponent modexps (r^n, c^(p-1))
+constexpr int kWinEnc = 5;       // window of the 32-bit engine's shared-exponent modexps (r^n, c^(p-1))
+constexpr int kWinSlide = 6;     // sliding window of the 27-bit engine's shared-exponent modexps
 constexpr int kWinMul = 4;       // window of the per-lane-exponent modexp (ct x pt)
 
 // Uniform key material, passed by value (lands in the kernarg segment -> SGPRs).
@@ -981,11 +982,11 @@ fphe_status launch_encrypt27(fphe_ctx* c, const uint32_t* P, uint32_t lp, const 
                              const uint32_t* r, const uint32_t key[8], uint64_t nonce, uint32_t* C, uint8_t* sign,
                              hipStream_t s) {
   constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = r27::LL * TPI, LDSW = NL > L ? NL : L, L1 = L / 2;
-  auto kern = k_encrypt27<L, kWinEnc>;
+  auto kern = k_encrypt27<L, kWinSlide>;
   const size_t lds = (size_t)kWavesPerBlock * LDSW * E * 4;
   set_lds(kern, lds);
   const unsigned grid = occ_grid(c, kern, lds, (count + E - 1) / E, "encrypt27");
-  const size_t tbytes = (size_t)grid * kWavesPerBlock * (1u << kWinEnc) * r27::LL * FPHE_WAVE * 4;
+  const size_t tbytes = (size_t)grid * kWavesPerBlock * kTabEntries<kWinSlide> * r27::LL * FPHE_WAVE * 4;
   const size_t rbytes = (size_t)ntiles_of(count) * L1 * FPHE_WAVE * 4;
   const bool draw = obf && !r;
   if (ensure_scratch(c, tbytes + (draw ? rbytes : 0)) != FPHE_OK) return FPHE_ERR_HIP;
@@ -1006,11 +1007,11 @@ fphe_status launch_encrypt27(fphe_ctx* c, const uint32_t* P, uint32_t lp, const 
 template <int L>
 fphe_status launch_decrypt27(fphe_ctx* c, const uint32_t* C, size_t count, uint32_t* P, hipStream_t s) {
   constexpr int TPI = L / 64, E = FPHE_WAVE / TPI, NL = r27::LL * TPI, LH = L / 2, LQ = L / 4;
-  auto kern = k_decrypt_pow27<L, kWinEnc>;
+  auto kern = k_decrypt_pow27<L, kWinSlide>;
   const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
   set_lds(kern, lds);
   const unsigned grid = occ_grid(c, kern, lds, (count + E - 1) / E, "decrypt_pow27");
-  const size_t tbytes = (size_t)grid * kWavesPerBlock * (1u << kWinEnc) * r27::LL * FPHE_WAVE * 4;
+  const size_t tbytes = (size_t)grid * kWavesPerBlock * kTabEntries<kWinSlide> * r27::LL * FPHE_WAVE * 4;
   const size_t ybytes = (size_t)ntiles_of(count) * 2 * LH * FPHE_WAVE * 4;
   if (ensure_scratch(c, tbytes + ybytes) != FPHE_OK) return FPHE_ERR_HIP;
   u32* Y = c->scratch + tbytes / 4;

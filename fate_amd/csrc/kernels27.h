@@ -11,6 +11,10 @@ namespace {
 
 using namespace fphe::r27;
 
+// window-table entries per wave for powm27<., W>: entry 0 for the caller + 2^(W-1) odd powers
+template <int W>
+constexpr u32 kTabEntries = 1u + (1u << (W - 1));
+
 // word w of element column `col` in a tile-major [.][rows][64] u32 tile: per-lane voffset
 __device__ __forceinline__ u32 tld(const __amdgpu_buffer_rsrc_t& r, u32 col, u32 w) {
   return __builtin_amdgcn_raw_buffer_load_b32(r, (col + 64u * w) * 4u, 0, 0);
@@ -47,36 +51,53 @@ __device__ __forceinline__ ColIO colio(const u32* tile_base, u32 rows, u32 col, 
   return c;
 }
 
-// Fixed-window modexp with a wave-uniform exponent (27-bit engine).  In: A = X in
-// Montgomery form (< 4N).  Out: X^E in Montgomery form (< 2N).
+// Sliding-window modexp with a wave-uniform exponent (27-bit engine).  In: A = X in
+// Montgomery form (< 2N).  Out: X^E in Montgomery form (< 2N).  Table entries
+// [1, 1 + 2^(W-1)) hold the odd powers X^1, X^3, ..., X^(2^W - 1); entry 0 stays free for
+// the caller.  The window schedule depends only on E, which is the same for every lane,
+// so it is computed on the scalar unit and control flow never diverges.  For E = n
+// (2048 bits, W = 6) this is ~2,373 products against 2,475 for the fixed w=5 window.
 template <int TPI, int W>
 __device__ __forceinline__ void powm27(L27& A, u32* bcol, u32 qoff, const Tile& tb, const Mod<TPI>& N,
                                        u32 np, const u32* __restrict__ Ex, int ebits, int q) {
+  constexpr u32 kOdd = 1u << (W - 1);
+  tab_store(tb, 1, A);                 // X
   to_slot<TPI>(bcol, qoff, A);
-  tab_store(tb, 1, A);
+  mont_mul<TPI>(A, bcol, N, np, q);    // X^2
+  to_slot<TPI>(bcol, qoff, A);         // slot = X^2 for the table build
+  tab_load(A, tb, 1);
 #pragma unroll 1
-  for (int k = 2; k < (1 << W); ++k) {
-    mont_mul<TPI>(A, bcol, N, np, q);
-    tab_store(tb, (u32)k, A);
+  for (u32 k = 1; k < kOdd; ++k) {
+    mont_mul<TPI>(A, bcol, N, np, q);  // X^(2k+1)
+    tab_store(tb, 1 + k, A);
   }
-  const int nwin = (ebits + W - 1) / W;
-  auto digit = [&](int w) -> u32 {
-    const int b0 = w * W;
-    const int limb = b0 >> 5, off = b0 & 31;
-    u32 v = Ex[limb] >> off;
-    if (off + W > 32) v |= Ex[limb + 1] << (32 - off);
-    return v & ((1u << W) - 1);
+  auto bit = [&](int i) -> u32 { return (Ex[i >> 5] >> (i & 31)) & 1u; };
+  // window [j, i]: the lowest set bit j >= i - W + 1, value odd
+  auto window = [&](int i, int& j) -> u32 {
+    j = i - W + 1 < 0 ? 0 : i - W + 1;
+    while (!bit(j)) ++j;
+    u32 v = 0;
+    for (int t = i; t >= j; --t) v = (v << 1) | bit(t);
+    return v;
   };
-  tab_load(A, tb, digit(nwin - 1));
+  int i = ebits - 1;
+  int j;
+  u32 v = window(i, j);
+  tab_load(A, tb, 1 + (v >> 1));
+  i = j - 1;
 #pragma unroll 1
-  for (int w = nwin - 2; w >= 0; --w) {
-#pragma unroll 1
-    for (int s = 0; s < W; ++s) sqr<TPI>(A, bcol, qoff, N, np, q);
-    const u32 d = digit(w);
-    if (d != 0) {
-      tab_to_slot<TPI>(bcol, qoff, tb, d);
-      mont_mul<TPI>(A, bcol, N, np, q);
+  while (i >= 0) {
+    if (!bit(i)) {
+      sqr<TPI>(A, bcol, qoff, N, np, q);
+      --i;
+      continue;
     }
+    v = window(i, j);
+#pragma unroll 1
+    for (int t = i; t >= j; --t) sqr<TPI>(A, bcol, qoff, N, np, q);
+    tab_to_slot<TPI>(bcol, qoff, tb, 1 + (v >> 1));
+    mont_mul<TPI>(A, bcol, N, np, q);
+    i = j - 1;
   }
 }
 
@@ -98,7 +119,8 @@ __global__ __launch_bounds__(kBlock) void k_encrypt27(KeyArgs K, const u32* __re
   const u32 gw = blockIdx.x * kWavesPerBlock + wib, nw = gridDim.x * kWavesPerBlock;
   u32* bcol = lds + wib * ldsw * E + g.e;
   const u32 qoff = lds_qoff<TPI>(g.q);
-  const Tile tb = make_tile(scratch + (size_t)gw * ((size_t)(1 << W) * LL * FPHE_WAVE), (1u << W) * LL * 256u, g.lane);
+  const Tile tb = make_tile(scratch + (size_t)gw * ((size_t)kTabEntries<W> * LL * FPHE_WAVE),
+                            kTabEntries<W> * LL * 256u, g.lane);
   Mod<TPI> N;
   N.init(K.N2_27, g.q);
   const u32 np = K.n2_np27;
@@ -201,7 +223,8 @@ __global__ __launch_bounds__(kBlock) void k_decrypt_pow27(KeyArgs K, const u32* 
   const u32 gw = blockIdx.x * kWavesPerBlock + wib, nw = gridDim.x * kWavesPerBlock;
   u32* bcol = lds + wib * ldsw * E + g.e;
   const u32 qoff = lds_qoff<TPI>(g.q);
-  const Tile tb = make_tile(scratch + (size_t)gw * ((size_t)(1 << W) * LL * FPHE_WAVE), (1u << W) * LL * 256u, g.lane);
+  const Tile tb = make_tile(scratch + (size_t)gw * ((size_t)kTabEntries<W> * LL * FPHE_WAVE),
+                            kTabEntries<W> * LL * 256u, g.lane);
   const u32 nwt = (u32)((count + E - 1) / E);
   for (u32 wt = gw; wt < nwt; wt += nw) {
     const size_t ebase = (size_t)wt * E;
@@ -349,15 +372,30 @@ __global__ __launch_bounds__(256) void k_mul_prep(KeyArgs K, const u32* __restri
     const bool isneg = (pneg[pe] != 0) && (any != 0);
     bool big = !isneg && (br_nmm == 0) && hi == 0;  // P >= n - max_int
     bool invalid = hi != 0 || (!isneg && !big && br_max != 0);
-    if (big) {  // exponent n - P (P > n would need a negative exponent: unreachable for encodings)
+    if (big) {  // exponent n - P
       u32 br = 0;
+      u32 D[L1];
 #pragma unroll
       for (int j = 0; j < L1; ++j) {
         const u64 d = (u64)K.n[j] - M[j] - br;
-        M[j] = (u32)d;
+        D[j] = (u32)d;
         br = (u32)(d >> 63);
       }
-      if (br) invalid = true;
+      if (br) {
+        // P > n: GMP powm(c^-1, n - P) with a negative exponent inverts the base again,
+        // i.e. c^(P - n): no inverse, exponent P - n
+        big = false;
+        br = 0;
+#pragma unroll
+        for (int j = 0; j < L1; ++j) {
+          const u64 d = (u64)M[j] - K.n[j] - br;
+          M[j] = (u32)d;
+          br = (u32)(d >> 63);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < L1; ++j) M[j] = D[j];
+      }
     }
     int eb = 0;
 #pragma unroll

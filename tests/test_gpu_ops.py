@@ -73,8 +73,10 @@ def test_sub_rsub(env):
 def test_decrypt_of_sub(env):
     """dec(enc(x) - enc(y)) == x - y (reference round-trip style, crates/paillier/src/lib.rs:190-197)."""
     fx, sk, pk, coder, opk, cts = env
-    x = torch.tensor(fx["encrypt"]["x_f32"][:48], dtype=torch.float64)
-    y = torch.tensor(fx["encrypt"]["x_f32"][48:96], dtype=torch.float64)
+    xs = fx["encrypt"]["x_f32"]
+    h = len(xs) // 2
+    x = torch.tensor(xs[:h], dtype=torch.float64)
+    y = torch.tensor(xs[h:2 * h], dtype=torch.float64)
     ex = pk.encrypt_encoded(coder.encode_f64_vec(x.cuda()), True)
     ey = pk.encrypt_encoded(coder.encode_f64_vec(y.cuda()), True)
     d = coder.decode_f64_vec(sk.decrypt_to_encoded(ex.sub(pk, ey))).cpu()
@@ -102,11 +104,16 @@ def test_mul_negative_and_big_plaintexts(env):
     assert host(pk, dev_vec(pk, c).mul(pk, pv)) == ref(want)
 
 
-def test_mul_invalid_plaintext_panics(env1024):
+def test_mul_plaintext_edges(env1024):
+    """Edges of Ciphertext::mul's classification (lib.rs:334-349).  For odd n,
+    max_int + 1 == n - max_int, so no significand below n is "invalid"; P > n takes the
+    inverse branch with a negative exponent, which GMP turns back into c^(P - n)."""
     fx, sk, pk, coder, opk, cts = env1024
-    pv = P.PlaintextVector.from_ints([opk.max_int + 1], [0])  # between max_int and n - max_int
-    with pytest.raises(P.PanicException):
-        dev_vec(pk, cts[:1]).mul(pk, pv)
+    sigs = [opk.max_int, opk.max_int + 1, opk.n - 1, opk.n, opk.n + 5, 0]
+    c = cts[:len(sigs)]
+    pv = P.PlaintextVector.from_ints(sigs, [0] * len(sigs))
+    want = [O.ct_mul(opk, x, O.Plaintext(s, 0)) for x, s in zip(c, sigs)]
+    assert host(pk, dev_vec(pk, c).mul(pk, pv)) == ref(want)
 
 
 def test_pack_squeeze(env1024):
