@@ -104,6 +104,21 @@ def cols_to_tiles(c: torch.Tensor) -> torch.Tensor:
     return c.reshape(L, nt, WAVE).permute(1, 0, 2).contiguous()
 
 
+def gather_rows(t: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+    """Elements idx of a tile-major [nt, L, 64] tensor as rows [len(idx), L] (only the
+    gathered elements move)."""
+    return t[idx // WAVE, :, idx % WAVE]
+
+
+def rows_to_tile_tensor(rows: torch.Tensor) -> torch.Tensor:
+    """[n, L] rows -> tile-major [ceil(n/64), L, 64] (zero padded)."""
+    n, L = rows.shape
+    nt = _ntiles(n)
+    if n != nt * WAVE:
+        rows = torch.cat([rows, rows.new_zeros((nt * WAVE - n, L))], dim=0)
+    return rows.reshape(nt, WAVE, L).permute(0, 2, 1).contiguous()
+
+
 def _pad_flat(x: torch.Tensor, n: int) -> torch.Tensor:
     nt = _ntiles(n)
     if x.shape[0] == nt * WAVE:
@@ -256,9 +271,8 @@ class PlaintextVector:
         return [Plaintext(self._gather(torch.tensor([i], device=self.device))) for i in range(self.count)]
 
     def _gather(self, idx: torch.Tensor) -> "PlaintextVector":
-        idx = idx.to(self.device)
-        cols = tiles_to_cols(self.P)[:, idx]
-        return PlaintextVector(cols_to_tiles(cols), _pad_flat(self.neg[idx], len(idx)),
+        idx = idx.to(self.device, torch.long)
+        return PlaintextVector(rows_to_tile_tensor(gather_rows(self.P, idx)), _pad_flat(self.neg[idx], len(idx)),
                                _pad_flat(self.exp[idx], len(idx)), len(idx))
 
     def __str__(self):
@@ -346,18 +360,19 @@ class CiphertextVector:
 
     # ---- element plumbing (torch indexing; no arithmetic) ---------------------------
     def _gather(self, idx: torch.Tensor) -> "CiphertextVector":
-        idx = idx.to(self.device)
-        cols = tiles_to_cols(self.C)[:, idx]
-        return CiphertextVector(cols_to_tiles(cols), _pad_flat(self.sign[idx], len(idx)),
+        idx = idx.to(self.device, torch.long)
+        return CiphertextVector(rows_to_tile_tensor(gather_rows(self.C, idx)), _pad_flat(self.sign[idx], len(idx)),
                                 _pad_flat(self.exp[idx], len(idx)), len(idx))
 
     def _assign(self, idx: torch.Tensor, src: "CiphertextVector") -> None:
-        idx = idx.to(self.device)
-        cols = tiles_to_cols(self.C)
-        cols[:, idx] = tiles_to_cols(src.C)[:, : src.count]
-        self.C = cols_to_tiles(cols)[: self.C.shape[0]]
-        self.sign[idx] = src.sign[: src.count]
-        self.exp[idx] = src.exp[: src.count]
+        """self[idx[i]] = src[i] (in place; only the assigned elements move)."""
+        idx = idx.to(self.device, torch.long)
+        if idx.numel() == 0:
+            return
+        srows = gather_rows(src.C, torch.arange(src.count, device=self.device)[: idx.numel()])
+        self.C[idx // WAVE, :, idx % WAVE] = srows
+        self.sign[idx] = src.sign[: idx.numel()]
+        self.exp[idx] = src.exp[: idx.numel()]
 
     def slice(self, start: int, size: int) -> "CiphertextVector":
         """``CiphertextVector::slice`` (lib.rs:452-455)."""
@@ -1064,9 +1079,13 @@ class Evaluator:
         vecs = [v for v in vec_list if v.count > 0]
         if not vecs:
             return CiphertextVector.zeros(0, vec_list[0].L2 if vec_list else 128)
-        cols = torch.cat([tiles_to_cols(v.C)[:, : v.count] for v in vecs], dim=1)
-        n = cols.shape[1]
-        return CiphertextVector(cols_to_tiles(cols),
+        n = sum(v.count for v in vecs)
+        if all(v.count % WAVE == 0 for v in vecs[:-1]):  # tile-aligned: concatenate tiles as they are
+            C = torch.cat([v.C[: _ntiles(v.count)] for v in vecs], dim=0)
+        else:
+            rows = torch.cat([v.C.permute(0, 2, 1).reshape(-1, v.C.shape[1])[: v.count] for v in vecs], dim=0)
+            C = rows_to_tile_tensor(rows)
+        return CiphertextVector(C,
                                 _pad_flat(torch.cat([v.sign[: v.count] for v in vecs]), n),
                                 _pad_flat(torch.cat([v.exp[: v.count] for v in vecs]), n), n)
 
