@@ -25,11 +25,13 @@ EF_DECODE_CORRUPTED = 0x02
 EF_DECODE_OVERFLOW = 0x04
 EF_MUL_INVALID_PT = 0x08
 EF_NOT_INVERTIBLE = 0x10
+EF_DECODE_I128 = 0x20
 
 # every symbol declared in include/fate_phe.h
 EXPORTED_SYMBOLS = (
     "fphe_ctx_create", "fphe_ctx_destroy", "fphe_ctx_limbs",
     "fphe_encode_f32", "fphe_encode_f64", "fphe_decode_f32", "fphe_decode_f64",
+    "fphe_encode_i64", "fphe_decode_i64", "fphe_decode_i32", "fphe_pack_f64", "fphe_unpack_f64",
     "fphe_encrypt", "fphe_decrypt", "fphe_add", "fphe_mul", "fphe_neg", "fphe_sqmul",
 )
 
@@ -69,6 +71,18 @@ def load() -> ctypes.CDLL:
             f = getattr(lib, name)
             f.argtypes = [vp, vp, ctypes.c_uint32, vp, ctypes.c_size_t, vp, vp, vp]
             f.restype = st
+        lib.fphe_encode_i64.argtypes = [vp, vp, ctypes.c_size_t, vp, vp, vp, vp]
+        lib.fphe_encode_i64.restype = st
+        for name in ("fphe_decode_i64", "fphe_decode_i32"):
+            f = getattr(lib, name)
+            f.argtypes = [vp, vp, ctypes.c_uint32, vp, ctypes.c_size_t, vp, vp, vp]
+            f.restype = st
+        lib.fphe_pack_f64.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                      vp, vp, vp, vp, vp]
+        lib.fphe_pack_f64.restype = st
+        lib.fphe_unpack_f64.argtypes = [vp, vp, ctypes.c_uint32, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32,
+                                        ctypes.c_uint32, ctypes.c_size_t, vp, vp]
+        lib.fphe_unpack_f64.restype = st
         lib.fphe_encrypt.argtypes = [vp, vp, ctypes.c_uint32, vp, ctypes.c_size_t, ctypes.c_int, vp,
                                      c_u32p, ctypes.c_uint64, vp, vp, vp]
         lib.fphe_encrypt.restype = st

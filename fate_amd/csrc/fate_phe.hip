@@ -795,6 +795,7 @@ __global__ __launch_bounds__(256) void k_decode_f64(KeyArgs K, const u32* __rest
 
 }  // namespace
 
+#include "codec_dev.h"
 #include "kernels27.h"
 
 // ======================================================================================
@@ -1298,6 +1299,82 @@ fphe_status fphe_decode_f64(const fphe_ctx* c, const uint32_t* P, uint32_t lp, c
   return hip_ok(hipGetLastError());
 }
 
+
+fphe_status fphe_encode_i64(const fphe_ctx* c, const int64_t* x, size_t count, uint32_t* P, uint8_t* neg,
+                            int32_t* exp, void* stream) {
+  if (!c) return FPHE_ERR_ARG;
+  if (count == 0) return FPHE_OK;
+  if (!x || !P || !neg || !exp) return FPHE_ERR_ARG;
+  DevGuard g(c->device);
+  const unsigned grid = (unsigned)std::min<size_t>((count + 255) / 256, (size_t)c->cus * 8);
+  if (c->L1 == 64)
+    hipLaunchKernelGGL(k_encode_i64<64>, dim3(grid), dim3(256), 0, (hipStream_t)stream, c->K, x, count, P, neg, exp);
+  else
+    hipLaunchKernelGGL(k_encode_i64<32>, dim3(grid), dim3(256), 0, (hipStream_t)stream, c->K, x, count, P, neg, exp);
+  return hip_ok(hipGetLastError());
+}
+
+fphe_status fphe_decode_i64(const fphe_ctx* c, const uint32_t* P, uint32_t lp, const int32_t* exp, size_t count,
+                            int64_t* out, int32_t* err, void* stream) {
+  if (!c || !err) return FPHE_ERR_ARG;
+  if (count == 0) return FPHE_OK;
+  if (!P || !exp || !out || lp == 0) return FPHE_ERR_ARG;
+  DevGuard g(c->device);
+  const unsigned grid = (unsigned)std::min<size_t>((count + 255) / 256, (size_t)c->cus * 8);
+  if (c->L1 == 64)
+    hipLaunchKernelGGL(k_decode_i64<64>, dim3(grid), dim3(256), 0, (hipStream_t)stream, c->K, P, lp, exp, count, out, err);
+  else
+    hipLaunchKernelGGL(k_decode_i64<32>, dim3(grid), dim3(256), 0, (hipStream_t)stream, c->K, P, lp, exp, count, out, err);
+  return hip_ok(hipGetLastError());
+}
+
+fphe_status fphe_decode_i32(const fphe_ctx* c, const uint32_t* P, uint32_t lp, const int32_t* exp, size_t count,
+                            int32_t* out, int32_t* err, void* stream) {
+  if (!c || !err) return FPHE_ERR_ARG;
+  if (count == 0) return FPHE_OK;
+  if (!P || !exp || !out || lp == 0) return FPHE_ERR_ARG;
+  DevGuard g(c->device);
+  const unsigned grid = (unsigned)std::min<size_t>((count + 255) / 256, (size_t)c->cus * 8);
+  if (c->L1 == 64)
+    hipLaunchKernelGGL(k_decode_i32<64>, dim3(grid), dim3(256), 0, (hipStream_t)stream, c->K, P, lp, exp, count, out, err);
+  else
+    hipLaunchKernelGGL(k_decode_i32<32>, dim3(grid), dim3(256), 0, (hipStream_t)stream, c->K, P, lp, exp, count, out, err);
+  return hip_ok(hipGetLastError());
+}
+
+fphe_status fphe_pack_f64(const fphe_ctx* c, const double* x, size_t count, uint32_t offset_bit, uint32_t pack_num,
+                          uint32_t precision, uint32_t* P, uint8_t* neg, int32_t* exp, int32_t* err, void* stream) {
+  if (!c || !err || pack_num == 0) return FPHE_ERR_ARG;
+  if (count == 0) return FPHE_OK;
+  if (!x || !P || !neg || !exp) return FPHE_ERR_ARG;
+  if ((uint64_t)offset_bit * pack_num > (uint64_t)32 * c->L1 + offset_bit) return FPHE_ERR_ARG;
+  DevGuard g(c->device);
+  const size_t nout = (count + pack_num - 1) / pack_num;
+  const unsigned grid = (unsigned)std::min<size_t>((nout + 63) / 64, (size_t)c->cus * 16);
+  if (c->L1 == 64)
+    hipLaunchKernelGGL(k_pack_f64<64>, dim3(grid), dim3(64), 0, (hipStream_t)stream, x, count, offset_bit, pack_num,
+                       precision, nout, P, neg, exp, err);
+  else
+    hipLaunchKernelGGL(k_pack_f64<32>, dim3(grid), dim3(64), 0, (hipStream_t)stream, x, count, offset_bit, pack_num,
+                       precision, nout, P, neg, exp, err);
+  return hip_ok(hipGetLastError());
+}
+
+fphe_status fphe_unpack_f64(const fphe_ctx* c, const uint32_t* P, uint32_t lp, size_t npacked, uint32_t offset_bit,
+                            uint32_t pack_num, uint32_t precision, size_t total, double* out, void* stream) {
+  if (!c || pack_num == 0 || offset_bit == 0 || offset_bit > 128) return FPHE_ERR_ARG;
+  if (npacked == 0 || total == 0) return FPHE_OK;
+  if (!P || !out || lp == 0) return FPHE_ERR_ARG;
+  DevGuard g(c->device);
+  const unsigned grid = (unsigned)std::min<size_t>((npacked + 255) / 256, (size_t)c->cus * 8);
+  if (c->L1 == 64)
+    hipLaunchKernelGGL(k_unpack_f64<64>, dim3(grid), dim3(256), 0, (hipStream_t)stream, P, lp, npacked, offset_bit,
+                       pack_num, precision, total, out);
+  else
+    hipLaunchKernelGGL(k_unpack_f64<32>, dim3(grid), dim3(256), 0, (hipStream_t)stream, P, lp, npacked, offset_bit,
+                       pack_num, precision, total, out);
+  return hip_ok(hipGetLastError());
+}
 
 fphe_status fphe_encrypt(fphe_ctx* c, const uint32_t* P, uint32_t lp, const uint8_t* neg, size_t count, int obf,
                          const uint32_t* r, const uint32_t rng_key[8], uint64_t nonce, uint32_t* C, uint8_t* sign,

@@ -207,6 +207,7 @@ _ERR_MESSAGES = [
     (_lib.EF_DECODE_OVERFLOW, "Overflow detected in decrypted number"),
     (_lib.EF_MUL_INVALID_PT, "invalid plaintext"),
     (_lib.EF_NOT_INVERTIBLE, "called `Option::unwrap()` on a `None` value (non-invertible)"),
+    (_lib.EF_DECODE_I128, "cant't convert to i128"),
 ]
 
 
@@ -951,33 +952,19 @@ class Coder:
         # encode_i64 / encode_i32 (lib.rs:68-78, 119-129): sig = v (v >= 0) or n + v, exp 0
         dev = _device(device if device is not None else (data.device if isinstance(data, torch.Tensor)
                                                          and data.is_cuda else None))
-        v = np.asarray(torch.as_tensor(data).detach().flatten().cpu().numpy(), dtype=np.int64)
-        n = v.size
-        L1 = self._key.L1
-        rows = np.zeros((n, L1), dtype=np.uint32)
-        nonneg = v >= 0
-        pos = v.astype(np.uint64)
-        rows[nonneg, 0] = (pos[nonneg] & 0xFFFFFFFF).astype(np.uint32)
-        rows[nonneg, 1] = (pos[nonneg] >> np.uint64(32)).astype(np.uint32)
-        negidx = np.nonzero(~nonneg)[0]
-        if negidx.size:
-            mag = (-(v[negidx].astype(object))).astype(object)
-            nl = ints_to_limbs([self.n], L1)[0].astype(np.int64)
-            m = np.array([int(x) for x in mag], dtype=object)
-            sub = np.zeros((negidx.size, L1), dtype=np.int64)
-            sub[:, 0] = np.array([int(x) & 0xFFFFFFFF for x in m], dtype=np.int64)
-            sub[:, 1] = np.array([int(x) >> 32 for x in m], dtype=np.int64)
-            br = np.zeros(negidx.size, dtype=np.int64)
-            res = np.zeros((negidx.size, L1), dtype=np.uint32)
-            for j in range(L1):
-                d = nl[j] - sub[:, j] - br
-                br = (d < 0).astype(np.int64)
-                res[:, j] = (d + (br << 32)).astype(np.uint32)
-            rows[negidx] = res
-        P = torch.from_numpy(rows_to_tiles(rows).view(np.int32)).to(dev)
+        x = torch.as_tensor(data).detach().flatten().to(dtype=torch.int64, device=dev).contiguous()
+        n = x.numel()
         nt = _ntiles(n)
-        return PlaintextVector(P, torch.zeros(nt * WAVE, dtype=torch.uint8, device=dev),
-                               torch.zeros(nt * WAVE, dtype=torch.int32, device=dev), n)
+        L1 = self._key.L1
+        out = PlaintextVector(torch.zeros((nt, L1, WAVE), dtype=torch.int32, device=dev),
+                              torch.zeros(nt * WAVE, dtype=torch.uint8, device=dev),
+                              torch.zeros(nt * WAVE, dtype=torch.int32, device=dev), n)
+        if n == 0:
+            return out
+        lib = _lib.load()
+        _lib.check(lib.fphe_encode_i64(self._key.ctx(dev), _ptr(x), n, _ptr(out.P), _ptr(out.neg), _ptr(out.exp),
+                                       ctypes.c_void_p(_stream(dev))), "fphe_encode_i64")
+        return out
 
     def encode_i64_vec(self, data, device=None) -> PlaintextVector:
         """``Coder.encode_i64_vec`` (paillier.rs:182-189)."""
@@ -1020,30 +1007,61 @@ class Coder:
             return sig - self.n
         raise PanicException("Overflow detected in decrypted number")
 
-    def decode_i64_vec(self, data: PlaintextVector) -> List[int]:
-        """``Coder.decode_i64_vec`` (paillier.rs:190-192; decode_i64 lib.rs:130-142)."""
-        sig, exps = data.to_ints()
-        out = []
-        for s, e in zip(sig, exps):
-            m = self._mantissa(s)
-            v = m << (4 * e) if e >= 0 else m >> (-4 * e)
-            if not -(1 << 127) <= v < (1 << 127):
-                raise PanicException("cant't convert to i128")
-            v &= (1 << 64) - 1
-            out.append(v - (1 << 64) if v >= (1 << 63) else v)
+    def _decode_int(self, data: PlaintextVector, dtype: torch.dtype) -> torch.Tensor:
+        dev = data.device
+        n = data.count
+        out = torch.empty(n, dtype=dtype, device=dev)
+        if n == 0:
+            return out
+        err = torch.zeros(1, dtype=torch.int32, device=dev)
+        lib = _lib.load()
+        fn = lib.fphe_decode_i64 if dtype == torch.int64 else lib.fphe_decode_i32
+        _lib.check(fn(self._key.ctx(dev), _ptr(data.P), data.P.shape[1], _ptr(data.exp), n, _ptr(out), _ptr(err),
+                      ctypes.c_void_p(_stream(dev))), "fphe_decode_int")
+        _raise_err(err)
         return out
 
+    def decode_i64_vec(self, data: PlaintextVector) -> List[int]:
+        """``Coder.decode_i64_vec`` (paillier.rs:190-192; decode_i64 lib.rs:130-142)."""
+        return self._decode_int(data, torch.int64).cpu().tolist()
+
     def decode_i32_vec(self, data: PlaintextVector) -> List[int]:
-        """``Coder.decode_i32_vec``: decode_f64 as i32 (saturating cast, lib.rs:143-146)."""
-        f = self.decode_f64_vec(data).cpu().tolist()
-        out = []
-        for x in f:
-            if x != x:
-                out.append(0)
-            else:
-                out.append(int(max(-(2 ** 31), min(2 ** 31 - 1, int(x) if abs(x) < 2 ** 63 else
-                                                   (2 ** 31 if x > 0 else -(2 ** 31))))))
+        """``Coder.decode_i32_vec`` (paillier.rs:201-203): decode_f64 as i32 (lib.rs:143-146)."""
+        return self._decode_int(data, torch.int32).cpu().tolist()
+
+    def pack_floats(self, float_tensor, offset_bit: int, pack_num: int, precision: int,
+                    device=None) -> PlaintextVector:
+        """``Coder.pack_floats`` (paillier.rs:135-138; lib.rs:79-93), on the device."""
+        dev = _device(device if device is not None else (float_tensor.device if isinstance(float_tensor, torch.Tensor)
+                                                         and float_tensor.is_cuda else None))
+        x = torch.as_tensor(float_tensor).detach().flatten().to(dtype=torch.float64, device=dev).contiguous()
+        n = (x.numel() + pack_num - 1) // pack_num
+        nt = _ntiles(n)
+        L1 = self._key.L1
+        out = PlaintextVector(torch.zeros((nt, L1, WAVE), dtype=torch.int32, device=dev),
+                              torch.zeros(nt * WAVE, dtype=torch.uint8, device=dev),
+                              torch.zeros(nt * WAVE, dtype=torch.int32, device=dev), n)
+        if n == 0:
+            return out
+        err = torch.zeros(1, dtype=torch.int32, device=dev)
+        lib = _lib.load()
+        _lib.check(lib.fphe_pack_f64(self._key.ctx(dev), _ptr(x), x.numel(), offset_bit, pack_num, precision,
+                                     _ptr(out.P), _ptr(out.neg), _ptr(out.exp), _ptr(err),
+                                     ctypes.c_void_p(_stream(dev))), "fphe_pack_f64")
+        _raise_err(err)
         return out
+
+    def unpack_floats(self, packed: PlaintextVector, offset_bit: int, pack_num: int, precision: int,
+                      total_num: int) -> List[float]:
+        """``Coder.unpack_floats`` (paillier.rs:140-142; lib.rs:94-118), on the device."""
+        dev = packed.device
+        out = torch.zeros(total_num, dtype=torch.float64, device=dev)
+        if total_num and packed.count:
+            lib = _lib.load()
+            _lib.check(lib.fphe_unpack_f64(self._key.ctx(dev), _ptr(packed.P), packed.P.shape[1], packed.count,
+                                           offset_bit, pack_num, precision, total_num, _ptr(out),
+                                           ctypes.c_void_p(_stream(dev))), "fphe_unpack_f64")
+        return out.cpu().tolist()
 
     # ---- scalars (length-1 vectors) ---------------------------------------------------
     def encode_f64(self, data: float) -> Plaintext:

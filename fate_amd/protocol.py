@@ -48,6 +48,14 @@ class Coder:
     def __init__(self, coder: _p.Coder):
         self.coder = coder
 
+    def pack_floats(self, float_tensor: V, offset_bit: int, pack_num: int, precision: int) -> FV:
+        """paillier.py:56-57 (device tensor in, no .tolist() round trip)."""
+        return self.coder.pack_floats(float_tensor.detach(), offset_bit, pack_num, precision)
+
+    def unpack_floats(self, packed: FV, offset_bit: int, pack_num: int, precision: int, total_num: int) -> V:
+        """paillier.py:59-60."""
+        return torch.tensor(self.coder.unpack_floats(packed, offset_bit, pack_num, precision, total_num))
+
     def encode_tensor(self, tensor: V, dtype: torch.dtype = None) -> FV:
         # paillier.py:68-69 encodes by tensor.dtype and ignores `dtype`
         return self.encode_vec(tensor.flatten(), dtype=tensor.dtype)

@@ -52,6 +52,7 @@ typedef enum {
 #define FPHE_EF_DECODE_OVERFLOW    0x04u  /* "Overflow detected in decrypted number" (lib.rs:177-179) */
 #define FPHE_EF_MUL_INVALID_PT     0x08u  /* "invalid plaintext" (lib.rs:342-343) */
 #define FPHE_EF_NOT_INVERTIBLE     0x10u  /* invert(...).unwrap() on a non-unit (math/src/rug/mod.rs:30-35) */
+#define FPHE_EF_DECODE_I128        0x20u  /* decode_i64: "cant't convert to i128" (lib.rs:130-142) */
 
 typedef struct fphe_ctx fphe_ctx;
 
@@ -83,6 +84,30 @@ fphe_status fphe_decode_f32(const fphe_ctx* ctx, const uint32_t* P, uint32_t lp,
                             size_t count, float* out, int32_t* err, void* stream);
 fphe_status fphe_decode_f64(const fphe_ctx* ctx, const uint32_t* P, uint32_t lp, const int32_t* exp,
                             size_t count, double* out, int32_t* err, void* stream);
+
+/* Device-side integer encode (Coder.encode_i64_vec / encode_i32_vec, paillier.rs:182-200;
+ * Coder::encode_i64, fixedpoint_paillier/src/lib.rs:68-78, 119-129): sig = v (v >= 0) or
+ * n + v, exp 0.  P is [T][L1][64]; i32 inputs are passed widened to int64. */
+fphe_status fphe_encode_i64(const fphe_ctx* ctx, const int64_t* x, size_t count, uint32_t* P, uint8_t* neg,
+                            int32_t* exp, void* stream);
+/* Device-side decode to int64 (Coder.decode_i64_vec, paillier.rs:190-192; Coder::decode_i64,
+ * lib.rs:130-142): (mantissa << 4 exp) with rug's floor shift for exp < 0, must fit i128
+ * (else FPHE_EF_DECODE_I128), then wraps to i64. */
+fphe_status fphe_decode_i64(const fphe_ctx* ctx, const uint32_t* P, uint32_t lp, const int32_t* exp, size_t count,
+                            int64_t* out, int32_t* err, void* stream);
+/* decode_i32 (lib.rs:143-146): decode_f64(...) as i32 (saturating, NaN -> 0). */
+fphe_status fphe_decode_i32(const fphe_ctx* ctx, const uint32_t* P, uint32_t lp, const int32_t* exp, size_t count,
+                            int32_t* out, int32_t* err, void* stream);
+/* Coder.pack_floats (paillier.rs:135-138; lib.rs:79-93): ceil(count/pack_num) plaintexts
+ * P [T][L1][64] (magnitude) + neg + exp(=0).  Scaled values must stay below 2^127. */
+fphe_status fphe_pack_f64(const fphe_ctx* ctx, const double* x, size_t count, uint32_t offset_bit,
+                          uint32_t pack_num, uint32_t precision, uint32_t* P, uint8_t* neg, int32_t* exp,
+                          int32_t* err, void* stream);
+/* Coder.unpack_floats (paillier.rs:140-142; lib.rs:94-118): `total` float64 outputs from
+ * npacked plaintexts P [T][lp][64]; offset_bit <= 128. */
+fphe_status fphe_unpack_f64(const fphe_ctx* ctx, const uint32_t* P, uint32_t lp, size_t npacked,
+                            uint32_t offset_bit, uint32_t pack_num, uint32_t precision, size_t total,
+                            double* out, void* stream);
 
 /* Encrypt encoded plaintexts: PK.encrypt_encoded (paillier.rs:51-57) ->
  * fixedpoint_paillier::PK::encrypt_encoded (lib.rs:370-381) -> paillier::PK::encrypt

@@ -201,3 +201,62 @@ def test_iadd_isub_vec_self(env1024):
             v = dev_vec(pk, data)
             (v.isub_vec_self if sub else v.iadd_vec_self)(sa, sb, size, pk)
             assert host(pk, v) == ref(_self_op_ref(opk, data, sa, sb, size, sub)), (sa, sb, size, sub)
+
+
+def test_int_codec(env):
+    """encode_i64 / decode_i64 / decode_i32 on the device vs the oracle (lib.rs:68-146)."""
+    fx, sk, pk, coder, opk, cts = env
+    vals = [0, 1, -1, 2**63 - 1, -2**63, 123456789012345, -987654321, 2**31, -2**31 - 5]
+    pv = coder.encode_i64_vec(torch.tensor(vals, dtype=torch.int64).cuda())
+    sig, exp = pv.to_ints()
+    assert sig == [O.encode_i64(opk.n, v).significant % opk.n for v in vals] and exp == [0] * len(vals)
+    assert coder.decode_i64_vec(pv) == [O.decode_i64(opk.n, s, 0) for s in sig]
+    # decode with exponents (the floor shift for negative mantissas, and i64 wrap of i128)
+    rng = random.Random(11)
+    ms = [rng.randrange(-(1 << 80), 1 << 80) for _ in range(40)] + [-7, 7, -(1 << 100), 5, 1 << 100, -(1 << 127)]
+    es = [rng.randrange(-8, 6) for _ in range(40)] + [-1, -1, -6, 30, 8, 0]
+    sigs = [m % opk.n for m in ms]
+    pv2 = P.PlaintextVector.from_ints(sigs, es)
+    want = []
+    for s_, e_ in zip(sigs, es):
+        try:
+            want.append(O.decode_i64(opk.n, s_, e_))
+        except OverflowError:
+            want.append(None)
+    ok = [i for i, w in enumerate(want) if w is not None]
+    pv_ok = P.PlaintextVector.from_ints([sigs[i] for i in ok], [es[i] for i in ok])
+    assert coder.decode_i64_vec(pv_ok) == [want[i] for i in ok]
+    bad = [i for i, w in enumerate(want) if w is None]
+    assert bad, "expected at least one out-of-range case"
+    with pytest.raises(P.PanicException):
+        coder.decode_i64_vec(P.PlaintextVector.from_ints([sigs[bad[0]]], [es[bad[0]]]))
+    # decode_i32: decode_f64 as i32 (saturating)
+    want32 = []
+    for s_, e_ in zip([sigs[i] for i in ok], [es[i] for i in ok]):
+        f = O.decode_f64(opk.n, s_, e_)
+        want32.append(0 if f != f else max(-2**31, min(2**31 - 1, int(f))) if abs(f) < 2**63 else
+                      (2**31 - 1 if f > 0 else -2**31))
+    assert coder.decode_i32_vec(pv_ok) == want32
+
+
+def test_pack_unpack_floats(env1024):
+    """pack_floats / unpack_floats on the device vs the oracle (lib.rs:79-118), SecureBoost
+    shape: g+1 and h packed at precision 52 with offset 77 (guest.py:203-206)."""
+    fx, sk, pk, coder, opk, cts = env1024
+    rng = random.Random(4)
+    vals = []
+    for _ in range(37):
+        g = rng.uniform(-1, 1)
+        vals += [g + 1.0, rng.uniform(0, 0.25)]
+    vals += [0.0, 2.0 ** -60, 1.5]  # ragged last chunk, a value that rounds to 0
+    off, pn, prec = 77, 2, 52
+    pv = coder.pack_floats(torch.tensor(vals, dtype=torch.float64).cuda(), off, pn, prec)
+    sig, exp = pv.to_ints()
+    want = O.pack_floats(vals, off, pn, prec)
+    assert sig == [w.significant for w in want] and exp == [0] * len(want)
+    got = coder.unpack_floats(pv, off, pn, prec, len(vals))
+    assert got == O.unpack_floats(want, off, pn, prec, len(vals))
+    # through encryption, ciphertext adds and pack_squeeze-free decryption
+    ct = pk.encrypt_encoded(pv, True)
+    back = coder.unpack_floats(sk.decrypt_to_encoded(ct), off, pn, prec, len(vals))
+    assert back == O.unpack_floats(want, off, pn, prec, len(vals))
