@@ -89,6 +89,19 @@ def dec_mac32_per_elem(key_bits: int) -> float:
     return 2 * (E + math.ceil(E / 5) + 16) * mac32_per_mont(L)
 
 
+def pmc_traffic_per_elem():
+    """HBM bytes per element of k_encrypt27 from the committed rocprofv3 PMC passes
+    (FETCH_SIZE and WRITE_SIZE in separate runs, FETCH_SIZE doubled per the calibration
+    probe tools/probe/fetch_calib.hip), or None when no such profile is present."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_encrypt27.json")))
+    if not paths:
+        return None, None
+    with open(paths[-1]) as f:
+        d = json.load(f)
+    return float(d["hbm_bytes_per_elem"]), os.path.relpath(paths[-1], ROOT)
+
+
 def cpu_baseline(p: int, q: int, seconds: float = 12.0):
     """libgmp restatement of the reference's per-element encrypt (oracle/gmp_ref.c)."""
     from oracle import gmp_ref
@@ -271,6 +284,7 @@ def main() -> None:
     hbm_bytes = N * (8 + 1 + 4 + key_bits // 4 + 1)
     r27 = os.environ.get("FPHE_ENGINE", "27") != "32"
     mad27 = N * enc_mad27_per_elem(key_bits, pk.n) / (enc_kernel_ms / 1e3) / 1e12
+    tb, tsrc = pmc_traffic_per_elem()
     roofline = {
         "bound": "valu",
         "kernel": "k_encrypt27<128,6> (+k_draw_r)" if r27 else "k_encrypt2<128,5> (+k_draw_r)",
@@ -278,7 +292,10 @@ def main() -> None:
         "peak": round(PEAK_TMAC32, 3),
         "unit": "TMAC32/s",
         "frac": round(achieved / PEAK_TMAC32, 4),
-        "traffic": None,
+        # HBM bytes per launch from PMC counters (separate --pmc runs, calibrated; dominated
+        # by the window-table scratch, see the profile's note); None if not profiled
+        "traffic": round(tb * N) if (tb is not None and r27) else None,
+        "traffic_source": tsrc if r27 else None,
         "per_elem_mac32": enc_mac32_per_elem(key_bits),
         "kernel_ms": round(enc_kernel_ms, 3),
         # instruction-issue view of the same launch: 27-bit-limb MACs issued (one

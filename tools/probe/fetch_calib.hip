@@ -1,0 +1,46 @@
+// Calibrates rocprofv3 FETCH_SIZE / WRITE_SIZE (gfx950) for the access pattern of the
+// modexp kernels' window table: one buffer_load_dword / buffer_store_dword per lane, a
+// wave touching one 256-byte row per instruction.  Reads and writes exactly BYTES bytes
+// (2 GiB, past the 256 MiB Infinity Cache) so the counters can be compared with a known
+// byte count.  Run under `rocprofv3 --pmc FETCH_SIZE` and, separately, `--pmc WRITE_SIZE`.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdint.h>
+
+constexpr size_t BYTES = 2ull << 30;
+
+__global__ __launch_bounds__(256) void k_read_rows(const uint32_t* buf, size_t nrows, uint32_t* sink) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(buf), 0, 0x7fffffff, 0x00020000);
+  const uint32_t lane = threadIdx.x & 63;
+  const size_t wave = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6), nwaves = (size_t)gridDim.x * 4;
+  uint32_t acc = 0;
+  for (size_t row = wave; row < nrows; row += nwaves) {
+    // rows are 256 B; address via a per-row base (the descriptor range covers 2 GiB - 1)
+    const uint32_t off = (uint32_t)(row * 256) + lane * 4;
+    acc += __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+  }
+  if (acc == 0x12345678u) sink[0] = acc;  // keep the loads alive
+}
+
+__global__ __launch_bounds__(256) void k_write_rows(uint32_t* buf, size_t nrows) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(buf, 0, 0x7fffffff, 0x00020000);
+  const uint32_t lane = threadIdx.x & 63;
+  const size_t wave = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6), nwaves = (size_t)gridDim.x * 4;
+  for (size_t row = wave; row < nrows; row += nwaves)
+    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)row, r, (uint32_t)(row * 256) + lane * 4, 0, 0);
+}
+
+int main() {
+  uint32_t *buf = nullptr, *sink = nullptr;
+  const size_t bytes = BYTES - 256;  // stay inside the 2^31-1 descriptor range
+  if (hipMalloc(&buf, BYTES) != hipSuccess || hipMalloc(&sink, 4) != hipSuccess) { printf("alloc failed\n"); return 1; }
+  const size_t nrows = bytes / 256;
+  hipLaunchKernelGGL(k_write_rows, dim3(2048), dim3(256), 0, 0, buf, nrows);   // dispatch 1: writes `bytes`
+  hipLaunchKernelGGL(k_read_rows, dim3(2048), dim3(256), 0, 0, buf, nrows, sink);  // dispatch 2: reads `bytes`
+  if (hipDeviceSynchronize() != hipSuccess) { printf("kernel failed\n"); return 1; }
+  printf("calibration: k_write_rows wrote %zu bytes, k_read_rows read %zu bytes (%.3f KiB each)\n", bytes, bytes,
+         bytes / 1024.0);
+  (void)hipFree(buf);
+  (void)hipFree(sink);
+  return 0;
+}
