@@ -51,12 +51,12 @@ def enc_products_per_elem(key_bits: int) -> int:
     return E + math.ceil(E / 5) + 16 + 1
 
 
-def sliding_window_products(e: int, w: int = 6) -> int:
-    """Montgomery products of powm27's sliding-window schedule for exponent e
-    (fate_amd/csrc/kernels27.h): table (1 square + 2^(w-1)-1 products), then one square per
-    bit below the first window and one product per later window."""
+def sliding_window_schedule(e: int, w: int = 6):
+    """(squarings, general products) of powm27's sliding-window schedule for exponent e
+    (fate_amd/csrc/kernels27.h): table build (X^2 as a general product + 2^(w-1)-1 products),
+    then one squaring per bit below the first window and one product per later window."""
     bits = [(e >> i) & 1 for i in range(e.bit_length())]
-    prods = 1 + (1 << (w - 1)) - 1
+    sq, mul = 0, 1 + (1 << (w - 1)) - 1
     i = len(bits) - 1
     j = max(i - w + 1, 0)
     while not bits[j]:
@@ -64,23 +64,32 @@ def sliding_window_products(e: int, w: int = 6) -> int:
     i = j - 1
     while i >= 0:
         if not bits[i]:
-            prods += 1
+            sq += 1
             i -= 1
             continue
         j = max(i - w + 1, 0)
         while not bits[j]:
             j += 1
-        prods += (i - j + 1) + 1
+        sq += i - j + 1
+        mul += 1
         i = j - 1
-    return prods
+    return sq, mul
+
+
+def sliding_window_products(e: int, w: int = 6) -> int:
+    sq, mul = sliding_window_schedule(e, w)
+    return sq + mul
 
 
 def enc_mad27_per_elem(key_bits: int, n: int) -> float:
-    # issued v_mad_u64_u32 of the reduced-radix engine (fate_amd/csrc/mont27_dev.h): a
-    # product over NL 27-bit limbs is NL rows x 2 NL MACs; NL = 152 for 4096-bit n^2.
+    # issued v_mad_u64_u32 of the reduced-radix engine (fate_amd/csrc/mont27_dev.h), summed
+    # over an element's TPI lanes: a general product is NL rows x 2 NL MACs; a squaring
+    # (mont_sqr) NL rows x TPI x (20 + 38) MACs.  NL = 152 for 4096-bit n^2.
     # Products: to-Montgomery, the sliding-window r^n, x C_nude.
     NL = 38 * (key_bits // 16 // 32)
-    return (1 + sliding_window_products(n) + 1) * 2 * NL * NL
+    TPI = NL // 38
+    sq, mul = sliding_window_schedule(n)
+    return (1 + mul + 1) * 2 * NL * NL + sq * NL * TPI * (20 + 38)
 
 
 def dec_mac32_per_elem(key_bits: int) -> float:

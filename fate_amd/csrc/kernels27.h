@@ -63,7 +63,7 @@ __device__ __forceinline__ void powm27(L27& A, u32* bcol, u32 qoff, const Tile& 
   constexpr u32 kOdd = 1u << (W - 1);
   tab_store(tb, 1, A);                 // X
   to_slot<TPI>(bcol, qoff, A);
-  mont_mul<TPI>(A, bcol, N, np, q);    // X^2
+  mont_mul<TPI>(A, bcol, N, np, q);    // X^2 (general product: keeps one unrolled squaring body)
   to_slot<TPI>(bcol, qoff, A);         // slot = X^2 for the table build
   tab_load(A, tb, 1);
 #pragma unroll 1
@@ -85,19 +85,27 @@ __device__ __forceinline__ void powm27(L27& A, u32* bcol, u32 qoff, const Tile& 
   u32 v = window(i, j);
   tab_load(A, tb, 1 + (v >> 1));
   i = j - 1;
+  // each step: the zero run, then the next window's squarings, then one table product.
+  // One squaring call site: mont_sqr is a 38-row unrolled body, kept once in the I-cache.
 #pragma unroll 1
   while (i >= 0) {
-    if (!bit(i)) {
-      sqr<TPI>(A, bcol, qoff, N, np, q);
+    int nsq = 0;
+    while (i >= 0 && !bit(i)) {
+      ++nsq;
       --i;
-      continue;
     }
-    v = window(i, j);
+    const bool mul = i >= 0;
+    if (mul) {
+      v = window(i, j);
+      nsq += i - j + 1;
+      i = j - 1;
+    }
 #pragma unroll 1
-    for (int t = i; t >= j; --t) sqr<TPI>(A, bcol, qoff, N, np, q);
-    tab_to_slot<TPI>(bcol, qoff, tb, 1 + (v >> 1));
-    mont_mul<TPI>(A, bcol, N, np, q);
-    i = j - 1;
+    for (int t = 0; t < nsq; ++t) sqr<TPI>(A, bcol, qoff, N, np, q);
+    if (mul) {
+      tab_to_slot<TPI>(bcol, qoff, tb, 1 + (v >> 1));
+      mont_mul<TPI>(A, bcol, N, np, q);
+    }
   }
 }
 
@@ -232,17 +240,15 @@ __global__ __launch_bounds__(kBlock) void k_decrypt_pow27(KeyArgs K, const u32* 
     const u32 col = (u32)(ebase & 63) + (u32)g.e;
     const u32* ctile = C + (size_t)tile * L32 * FPHE_WAVE;
     u32* ytile = Y + (size_t)tile * 2 * L1 * FPHE_WAVE;
-    L27 A;
-    dec_half27<TPI, W>(ctile, col, L32, bcol, qoff, tb, K.P2_27, K.p2_np27, K.P2R1_27, K.P2R2_27, K.pm1,
-                       K.pm1_bits, g.q, A);
-    {
-      const ColIO Yo = colio(ytile, 2 * L1, col, 32u * g.q);
-      store_chunk<TPI>(A, g.q, [&](int k, u32 v) { Yo.st(k, v); });
-    }
-    dec_half27<TPI, W>(ctile, col, L32, bcol, qoff, tb, K.Q2_27, K.q2_np27, K.Q2R1_27, K.Q2R2_27, K.qm1,
-                       K.qm1_bits, g.q, A);
-    {
-      const ColIO Yo = colio(ytile, 2 * L1, col, L1 + 32u * g.q);
+    // the two halves in a rolled loop: one inlined copy of the modexp (I-cache)
+#pragma unroll 1
+    for (u32 h = 0; h < 2; ++h) {
+      const bool hq = h != 0;
+      L27 A;
+      dec_half27<TPI, W>(ctile, col, L32, bcol, qoff, tb, hq ? K.Q2_27 : K.P2_27, hq ? K.q2_np27 : K.p2_np27,
+                         hq ? K.Q2R1_27 : K.P2R1_27, hq ? K.Q2R2_27 : K.P2R2_27, hq ? K.qm1 : K.pm1,
+                         hq ? K.qm1_bits : K.pm1_bits, g.q, A);
+      const ColIO Yo = colio(ytile, 2 * L1, col, h * L1 + 32u * g.q);
       store_chunk<TPI>(A, g.q, [&](int k, u32 v) { Yo.st(k, v); });
     }
   }

@@ -46,6 +46,8 @@ struct L27 {
   __device__ __forceinline__ void set2(int k, u32 lo, u32 hi) { p[k] = ((u64)hi << 32) | lo; }
 };
 
+#include "mont27_sq_gen.h"
+
 template <int TPI>
 struct Geo {
   static constexpr int E = FPHE_WAVE / TPI;  // elements per wave
@@ -155,6 +157,26 @@ __device__ __forceinline__ void normalize_almost(const u64 (&T)[LL], L27& A, int
   }
 }
 
+// One reduction row: m = T_0 n' mod 2^27 (broadcast from the element's lane 0), then
+// T = (T + m N) / 2^27 with the word leaving each lane's bottom limb passed to the top limb
+// of the lane below.
+template <int TPI>
+__device__ __forceinline__ void red_row(u64 (&T)[LL], const Mod<TPI>& N, const u32 nprime, int q) {
+  const u32 m = dpp_bcast<TPI>(((u32)T[0] * nprime) & MASK);
+  // X = m N_0 + T_0 ; T_{j-1} = m N_j + T_j  (the shift by one limb)
+  u64 X;
+  if constexpr (TPI > 1) {
+    asm volatile(R27_ASM_REDROW : [x] "=&v"(X), R27_T_OPS(T) : [m] "v"(m), R27_N_INS(N, "v") : "vcc", "memory");
+    T[0] += (q == 0) ? (X >> LB) : 0ull;  // lowest limb: X = 0 mod 2^27
+    const u64 up = dpp_from_next64(X);     // X of the lane above
+    T[LL - 1] = (q == TPI - 1) ? 0ull : up;
+  } else {
+    asm volatile(R27_ASM_REDROW : [x] "=&v"(X), R27_T_OPS(T) : [m] "v"(m), R27_N_INS(N, "s") : "vcc", "memory");
+    T[0] += X >> LB;
+    T[LL - 1] = 0;
+  }
+}
+
 template <int TPI>
 __device__ __forceinline__ void mont_mul(L27& A, const u32* bcol, const Mod<TPI>& N, const u32 nprime, int q) {
   constexpr int E = Geo<TPI>::E, NL = Geo<TPI>::NL;
@@ -168,20 +190,62 @@ __device__ __forceinline__ void mont_mul(L27& A, const u32* bcol, const Mod<TPI>
     // b_{i+1} between the two row blocks so its latency hides under the reduction row.
     asm volatile(R27_ASM_OPROW : R27_T_OPS(T) : R27_A_INS(A), [b] "v"(b) : "vcc", "memory");
     const u32 bn = bcol[(i + 1 < NL ? i + 1 : 0) * E];
-    const u32 m = dpp_bcast<TPI>(((u32)T[0] * nprime) & MASK);
-    // X = m N_0 + T_0 ; T_{j-1} = m N_j + T_j  (the shift by one limb)
-    u64 X;
-    if constexpr (TPI > 1) {
-      asm volatile(R27_ASM_REDROW : [x] "=&v"(X), R27_T_OPS(T) : [m] "v"(m), R27_N_INS(N, "v") : "vcc", "memory");
-      T[0] += (q == 0) ? (X >> LB) : 0ull;  // lowest limb: X = 0 mod 2^27
-      const u64 up = dpp_from_next64(X);     // X of the lane above
-      T[LL - 1] = (q == TPI - 1) ? 0ull : up;
-    } else {
-      asm volatile(R27_ASM_REDROW : [x] "=&v"(X), R27_T_OPS(T) : [m] "v"(m), R27_N_INS(N, "s") : "vcc", "memory");
-      T[0] += X >> LB;
-      T[LL - 1] = 0;
-    }
+    red_row<TPI>(T, N, nprime, q);
     b = bn;
+  }
+  normalize_almost<TPI>(T, A, q);
+}
+
+// ---- A <- A^2 R^-1 (mod N), lazy: half the operand MACs ----------------------------------
+// The square needs each unordered limb pair {i, k} once (doubled) and each diagonal a_i^2
+// once.  In the shifted CIOS frame, row i adds a_i a_k at position k, and the same pair can
+// equally be added by row k at position i.  Positions are fixed to lanes (lane q holds
+// [38q, 38q + 38)), and a SIMD row costs the MOST MACs any lane does, so the pairs are
+// split to give every lane the same 20-position window per row: row i = 38 s + a (slice s,
+// local index a) touches the lane-local positions (a + t) mod 38, t = 0..19, with multiplier
+//   t = 0     : 2 a_i if q > s,  a_i if q == s (the diagonal),  0 if q < s
+//   t = 1..18 : 2 a_i
+//   t = 19    : 2 a_i if q < s,  2 a_i if q == s and a < 19,     0 otherwise.
+// Pair (x in slice X, y in slice Y, X < Y, local xa, yb) is then added by row x iff
+// (yb - xa) mod 38 in [0, 19) and by row y iff it is in [19, 38); a diagonal-block pair
+// a < b by row a iff b - a <= 19, else by row b.  Exactly once either way.  Rows are
+// unrolled by 38 so the window's register indices are compile-time; 20 + 38 MACs per row
+// against 38 + 38.  Bounds: 2 a_i a_k < 2^55.01 and an absolute column receives <= 77
+// operand and <= NL reduction products, < 2^62.3 (the mont_mul bound).
+template <int TPI, int a>
+__device__ __forceinline__ void sq_rows(u64 (&T)[LL], const L27& A, u32& b, const u32* bs, const u32* bnext,
+                                        u32 shf, u32 mkf, u32 mkl0, u32 mkl1, const Mod<TPI>& N, u32 nprime,
+                                        int q) {
+  constexpr int E = Geo<TPI>::E;
+  const u32 b2 = b << 1;
+  const u32 bf = (b << shf) & mkf;
+  const u32 bl = b2 & (a < LL / 2 ? mkl0 : mkl1);
+  r27_sqrow<a>(T, A, bf, b2, bl);
+  u32 bn;
+  if constexpr (a + 1 < LL) bn = bs[(a + 1) * E];
+  else bn = bnext[0];
+  red_row<TPI>(T, N, nprime, q);
+  b = bn;
+  if constexpr (a + 1 < LL) sq_rows<TPI, a + 1>(T, A, b, bs, bnext, shf, mkf, mkl0, mkl1, N, nprime, q);
+}
+
+// bcol must hold A (to_slot) -- sqr() below does that.
+template <int TPI>
+__device__ __forceinline__ void mont_sqr(L27& A, const u32* bcol, const Mod<TPI>& N, const u32 nprime, int q) {
+  constexpr int E = Geo<TPI>::E;
+  u64 T[LL];
+#pragma unroll
+  for (int j = 0; j < LL; ++j) T[j] = 0;
+  u32 b = bcol[0];
+#pragma unroll 1
+  for (int s = 0; s < TPI; ++s) {
+    const u32 shf = q > s ? 1u : 0u;
+    const u32 mkf = q >= s ? ~0u : 0u;
+    const u32 mkl0 = q <= s ? ~0u : 0u;
+    const u32 mkl1 = q < s ? ~0u : 0u;
+    const u32* bs = bcol + s * LL * E;
+    const u32* bnext = s + 1 < TPI ? bs + LL * E : bcol;
+    sq_rows<TPI, 0>(T, A, b, bs, bnext, shf, mkf, mkl0, mkl1, N, nprime, q);
   }
   normalize_almost<TPI>(T, A, q);
 }
@@ -218,7 +282,7 @@ __device__ __forceinline__ void one_to_slot(u32* bcol, u32 qoff, int q) {
 template <int TPI>
 __device__ __forceinline__ void sqr(L27& A, u32* bcol, u32 qoff, const Mod<TPI>& N, u32 np, int q) {
   to_slot<TPI>(bcol, qoff, A);
-  mont_mul<TPI>(A, bcol, N, np, q);
+  mont_sqr<TPI>(A, bcol, N, np, q);
 }
 
 // per-lane table in global scratch: entry k, limb j at byte (k*LL + j)*256 (+ lane*4)
