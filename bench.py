@@ -92,6 +92,14 @@ def enc_mad27_per_elem(key_bits: int, n: int) -> float:
     return (1 + mul + 1) * 2 * NL * NL + sq * NL * TPI * (20 + 38)
 
 
+def enc_crt_mac32_per_elem(key_bits: int) -> float:
+    # key-holder encrypt: two E-bit-exponent modexps over the L/2-limb p^2, q^2 (E = bits of
+    # n mod s(s-1), ~key_bits), w=5 fixed-window formula of SURVEY.md §8(d), + 4 products
+    # of the recombination over n^2
+    E = key_bits
+    return 2 * (E + math.ceil(E / 5) + 16) * mac32_per_mont(key_bits // 32) + 4 * mac32_per_mont(key_bits // 16)
+
+
 def dec_mac32_per_elem(key_bits: int) -> float:
     E = key_bits // 2
     L = key_bits // 32
@@ -158,7 +166,10 @@ def main() -> None:
     with open(KEY_FIXTURE) as f:
         fx = json.load(f)
     p, q = int(fx["p"], 16), int(fx["q"], 16)
-    sk, pk, coder = P.keypair_from_primes(p, q)
+    # the headline is the public-key path (what paillier::PK::encrypt computes from n alone);
+    # pk_kh is the key-holder PK that keygen hands the party owning the private key
+    sk, pk, coder = P.keypair_from_primes(p, q, keyholder=False)
+    pk_kh = P.keypair_from_primes(p, q, keyholder=True)[1]
     key_bits = pk.n.bit_length()
 
     N = args.n
@@ -268,7 +279,30 @@ def main() -> None:
             want[:, 1].index_add_(0, positions[:, f], xh)
         fin = torch.isfinite(want)
         hist_ok = bool(torch.allclose(hd[fin], want[fin], rtol=1e-9, atol=1e-6))
+        # key-holder encryption (CRT halves): throughput, round trip, and identity with the
+        # public-key path on a subset with the same injected r
+        torch.cuda.synchronize(dev)
+        e0.record(stream)
+        ck = pk_kh.encrypt_encoded(coder.encode_f32_vec(xd), True)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        crt_ms = e0.elapsed_time(e1)
+        yk = coder.decode_f32_vec(sk.decrypt_to_encoded(ck))
+        crt_roundtrip = bool(np.array_equal(yk.cpu().numpy().view(np.uint32), xb))
+        nsub = min(N, 4096)
+        rr = np.random.default_rng(5 + rank)
+        rsub = [1 + int.from_bytes(rr.bytes(key_bits // 8), "little") % (pk.n - 1) for _ in range(nsub)]
+        psub = coder.encode_f32_vec(xd[:nsub])
+        cpub = pk.encrypt_encoded(psub, True, r=rsub)
+        ckh = pk_kh.encrypt_encoded(psub, True, r=rsub)
+        crt_same = bool(torch.equal(cpub.C, ckh.C) and torch.equal(cpub.sign, ckh.sign))
+        del ck, yk, cpub, ckh
         extras = {
+            "encrypt_keyholder_crt_per_s": round(N / (crt_ms / 1e3), 1),
+            "encrypt_keyholder_crt_roofline_frac": round(N * enc_crt_mac32_per_elem(key_bits) / (crt_ms / 1e3) / 1e12
+                                                         / PEAK_TMAC32, 4),
+            "encrypt_keyholder_crt_roundtrip_bit_exact": crt_roundtrip,
+            "encrypt_keyholder_crt_equals_public_4096": crt_same,
             "ct_mul_per_s": round(N / (mul_ms / 1e3), 1),
             "histogram_scatter_adds_per_s": round(N * HF * 2 / hist_s, 1),
             "histogram_config": f"{N} samples x {HF} features x {NB} bins x (g,h), iupdate fold on device",

@@ -32,7 +32,7 @@ EXPORTED_SYMBOLS = (
     "fphe_ctx_create", "fphe_ctx_destroy", "fphe_ctx_limbs",
     "fphe_encode_f32", "fphe_encode_f64", "fphe_decode_f32", "fphe_decode_f64",
     "fphe_encode_i64", "fphe_decode_i64", "fphe_decode_i32", "fphe_pack_f64", "fphe_unpack_f64",
-    "fphe_encrypt", "fphe_decrypt", "fphe_add", "fphe_mul", "fphe_neg", "fphe_sqmul",
+    "fphe_encrypt", "fphe_encrypt_crt", "fphe_decrypt", "fphe_add", "fphe_mul", "fphe_neg", "fphe_sqmul",
 )
 
 _lock = threading.Lock()
@@ -86,6 +86,9 @@ def load() -> ctypes.CDLL:
         lib.fphe_encrypt.argtypes = [vp, vp, ctypes.c_uint32, vp, ctypes.c_size_t, ctypes.c_int, vp,
                                      c_u32p, ctypes.c_uint64, vp, vp, vp]
         lib.fphe_encrypt.restype = st
+        lib.fphe_encrypt_crt.argtypes = [vp, vp, ctypes.c_uint32, vp, ctypes.c_size_t, vp, c_u32p, ctypes.c_uint64,
+                                         vp, vp, vp]
+        lib.fphe_encrypt_crt.restype = st
         lib.fphe_decrypt.argtypes = [vp, vp, ctypes.c_size_t, vp, vp]
         lib.fphe_decrypt.restype = st
         lib.fphe_add.argtypes = [vp, vp, vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_size_t, vp, vp, vp, vp]

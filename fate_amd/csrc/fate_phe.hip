@@ -52,6 +52,11 @@ struct KeyArgs {
   u32 n2_np27, p2_np27, q2_np27;                             // -N^{-1} mod 2^27
   const u32* Nn_27; const u32* NnR1_27; const u32* NnR2_27;  // n, R mod n, R^2 mod n    [NLh]
   u32 nn_np27, nn_inv27;                                     // -n^{-1}, n^{-1} mod 2^27
+  // key-holder (CRT) encryption, valid iff has_sk: r^n mod s^2 = r^(n mod s(s-1)) mod s^2,
+  // recombined as x_p Kp + x_q Kq mod n^2 (Kp = q^2 (q^-2 mod p^2), Kq = p^2 (p^-2 mod q^2))
+  const u32* ep; const u32* eq;          // n mod p(p-1), n mod q(q-1)           [L1]
+  int ep_bits, eq_bits;
+  const u32* KpR_27; const u32* KqR_27;  // Kp R, Kq R mod n^2 (27-bit, R = 2^(27 NL2)) [NL2]
 };
 
 __device__ __forceinline__ void set_err(int32_t* err, u32 f) {
@@ -455,7 +460,7 @@ __global__ __launch_bounds__(kBlock) void k_decrypt(KeyArgs K, const u32* __rest
   }
 }
 
-// decrypt, CRT phase for the reduced-radix path: y_p, y_q (k_decrypt_pow27) -> m.
+// decrypt, CRT phase for the reduced-radix path: y_p, y_q (k_pow_half27<., ., false>) -> m.
 template <int L>
 __global__ __launch_bounds__(kBlock) void k_decrypt_crt(KeyArgs K, const u32* __restrict__ Y, u32 ntiles,
                                                         u32* __restrict__ Pout) {
@@ -1008,7 +1013,7 @@ fphe_status launch_encrypt27(fphe_ctx* c, const uint32_t* P, uint32_t lp, const 
 template <int L>
 fphe_status launch_decrypt27(fphe_ctx* c, const uint32_t* C, size_t count, uint32_t* P, hipStream_t s) {
   constexpr int TPI = L / 64, E = FPHE_WAVE / TPI, NL = r27::LL * TPI, LH = L / 2, LQ = L / 4;
-  auto kern = k_decrypt_pow27<L, kWinSlide>;
+  auto kern = k_pow_half27<L, kWinSlide, false>;
   const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
   set_lds(kern, lds);
   const unsigned grid = occ_grid(c, kern, lds, (count + E - 1) / E, "decrypt_pow27");
@@ -1022,6 +1027,41 @@ fphe_status launch_decrypt27(fphe_ctx* c, const uint32_t* C, size_t count, uint3
   set_lds(kcrt, lds2);
   const unsigned grid2 = grid_for(c, count, bpc_for_slot(LQ));
   hipLaunchKernelGGL(kcrt, dim3(grid2), dim3(kBlock), lds2, s, c->K, Y, ntiles_of(count), P);
+  return hip_ok(hipGetLastError());
+}
+
+// key-holder encryption: r^n mod p^2 and mod q^2 (half-size modexps), then the CRT
+// recombination times the nude ciphertext.  Same integers as launch_encrypt27.
+template <int L>
+fphe_status launch_encrypt_crt27(fphe_ctx* c, const uint32_t* P, uint32_t lp, const uint8_t* neg, size_t count,
+                                 const uint32_t* r, const uint32_t key[8], uint64_t nonce, uint32_t* C,
+                                 uint8_t* sign, hipStream_t s) {
+  constexpr int TPIh = L / 64, Eh = FPHE_WAVE / TPIh, NLh = r27::LL * TPIh, L1 = L / 2;
+  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = r27::LL * TPI, LDSW = NL > L + 2 ? NL : L + 2;
+  auto k1 = k_pow_half27<L, kWinSlide, true>;
+  const size_t lds1 = (size_t)kWavesPerBlock * NLh * Eh * 4;
+  set_lds(k1, lds1);
+  const unsigned g1 = occ_grid(c, k1, lds1, (count + Eh - 1) / Eh, "pow_half27<enc>");
+  const size_t tbytes = (size_t)g1 * kWavesPerBlock * kTabEntries<kWinSlide> * r27::LL * FPHE_WAVE * 4;
+  const size_t ybytes = (size_t)ntiles_of(count) * 2 * L1 * FPHE_WAVE * 4;
+  const size_t rbytes = (size_t)ntiles_of(count) * L1 * FPHE_WAVE * 4;
+  if (ensure_scratch(c, tbytes + ybytes + (r ? 0 : rbytes)) != FPHE_OK) return FPHE_ERR_HIP;
+  u32* Y = c->scratch + tbytes / 4;
+  const u32* rbuf = r;
+  if (!r) {
+    u32* rdev = Y + ybytes / 4;
+    ChaChaKey ck;
+    for (int i = 0; i < 8; ++i) ck.k[i] = key[i];
+    const unsigned rgrid = (unsigned)std::min<size_t>((count + 255) / 256, (size_t)c->cus * 4);
+    hipLaunchKernelGGL(k_draw_r<L1>, dim3(rgrid), dim3(256), 0, s, c->K, count, ck, nonce, rdev);
+    rbuf = rdev;
+  }
+  hipLaunchKernelGGL(k1, dim3(g1), dim3(kBlock), lds1, s, c->K, rbuf, count, Y, c->scratch, (u32)NLh);
+  auto k2 = k_encrypt_crt27<L>;
+  const size_t lds2 = (size_t)kWavesPerBlock * LDSW * E * 4;
+  set_lds(k2, lds2);
+  const unsigned g2 = occ_grid(c, k2, lds2, (count + E - 1) / E, "encrypt_crt27");
+  hipLaunchKernelGGL(k2, dim3(g2), dim3(kBlock), lds2, s, c->K, P, lp, neg, count, Y, C, sign, (u32)LDSW);
   return hip_ok(hipGetLastError());
 }
 
@@ -1148,7 +1188,8 @@ fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, 
     size_t o_P2 = 0, o_P2R3 = 0, o_pm1 = 0, o_p = 0, o_pinv2 = 0, o_hpR = 0;
     size_t o_Q2 = 0, o_Q2R3 = 0, o_qm1 = 0, o_q = 0, o_qinv2 = 0, o_hqR = 0, o_pinvqR = 0;
     u32 p2n0 = 0, pn0 = 0, q2n0 = 0, qn0 = 0;
-    int pm1b = 0, qm1b = 0;
+    int pm1b = 0, qm1b = 0, epb = 0, eqb = 0;
+    size_t o_ep = 0, o_eq = 0, o_KpR = 0, o_KqR = 0;
     const bool has_sk = p_w != nullptr;
     if (has_sk) {
       Limbs p = from_words(p_w, LQ), q = from_words(q_w, LQ);
@@ -1188,6 +1229,16 @@ fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, 
       p2n0 = hbn::neg_inv32(P2[0]); pn0 = hbn::neg_inv32(p[0]);
       q2n0 = hbn::neg_inv32(Q2[0]); qn0 = hbn::neg_inv32(q[0]);
       pm1b = (int)hbn::bitlen(pm1); qm1b = (int)hbn::bitlen(qm1);
+      // CRT encryption constants
+      Limbs ep = hbn::mod(n, hbn::mul(p, pm1)), eq = hbn::mod(n, hbn::mul(q, qm1));
+      o_ep = put(ep, L1);
+      o_eq = put(eq, L1);
+      epb = (int)hbn::bitlen(ep); eqb = (int)hbn::bitlen(eq);
+      const Limbs R27 = hbn::pow2_mod((size_t)27 * NL2, N2);
+      const Limbs Kp = hbn::mul(Q2, hbn::inv_mod(hbn::mod(Q2, P2), P2));  // < n^2
+      const Limbs Kq = hbn::mul(P2, hbn::inv_mod(hbn::mod(P2, Q2), Q2));
+      o_KpR = put(to27(hbn::mod(hbn::mul(Kp, R27), N2), NL2), NL2);
+      o_KqR = put(to27(hbn::mod(hbn::mul(Kq, R27), N2), NL2), NL2);
     }
     auto* c = new fphe_ctx();
     c->device = device; c->key_bits = key_bits; c->L1 = L1; c->L2 = L2; c->LQ = LQ; c->has_sk = has_sk;
@@ -1223,6 +1274,8 @@ fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, 
       K.P2_27 = b + o_P2_27; K.P2R1_27 = b + o_P2R1_27; K.P2R2_27 = b + o_P2R2_27;
       K.Q2_27 = b + o_Q2_27; K.Q2R1_27 = b + o_Q2R1_27; K.Q2R2_27 = b + o_Q2R2_27;
       K.p2_np27 = p2n0 & ((1u << 27) - 1u); K.q2_np27 = q2n0 & ((1u << 27) - 1u);
+      K.ep = b + o_ep; K.eq = b + o_eq; K.ep_bits = epb; K.eq_bits = eqb;
+      K.KpR_27 = b + o_KpR; K.KqR_27 = b + o_KqR;
     }
     *out = c;
     return FPHE_OK;
@@ -1393,6 +1446,23 @@ fphe_status fphe_encrypt(fphe_ctx* c, const uint32_t* P, uint32_t lp, const uint
   }
   if (c->L2 == 128) return launch_encrypt<128>(c, P, lp, neg, count, obf, r, rng_key, nonce, C, sign, (hipStream_t)stream);
   return launch_encrypt<64>(c, P, lp, neg, count, obf, r, rng_key, nonce, C, sign, (hipStream_t)stream);
+}
+
+
+fphe_status fphe_encrypt_crt(fphe_ctx* c, const uint32_t* P, uint32_t lp, const uint8_t* neg, size_t count,
+                             const uint32_t* r, const uint32_t rng_key[8], uint64_t nonce, uint32_t* C,
+                             uint8_t* sign, void* stream) {
+  if (!c) return FPHE_ERR_ARG;
+  if (!c->has_sk) return FPHE_ERR_NO_SK;
+  if (count == 0) return FPHE_OK;
+  if (!P || !neg || !C || !sign || lp == 0 || lp > (uint32_t)c->L1) return FPHE_ERR_ARG;
+  if (count >= (1ull << 32)) return FPHE_ERR_ARG;
+  if (!r && !rng_key) return FPHE_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DevGuard g(c->device);
+  if (c->L2 == 128)
+    return launch_encrypt_crt27<128>(c, P, lp, neg, count, r, rng_key, nonce, C, sign, (hipStream_t)stream);
+  return launch_encrypt_crt27<64>(c, P, lp, neg, count, r, rng_key, nonce, C, sign, (hipStream_t)stream);
 }
 
 

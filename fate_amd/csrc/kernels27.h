@@ -173,15 +173,19 @@ __global__ __launch_bounds__(kBlock) void k_encrypt27(KeyArgs K, const u32* __re
 }
 
 // ======================================================================================
-// decrypt, modexp phase: y_s = c^(s-1) mod s^2 for s in {p, q} (paillier/src/lib.rs:174-176,
-// the pow_mod of h_function), written as 32-bit words to Y[tile][2*L1][64] (y_p rows
-// [0,L1), y_q rows [L1, 2L1)).  The CRT tail runs in k_decrypt_crt.
+// Half-size modexps mod p^2 and q^2 (TPI = 2 for 2048-bit keys), two uses:
+//  decrypt (ENC = false): y_s = c^(s-1) mod s^2 for s in {p, q} (paillier/src/lib.rs:174-176,
+//    the pow_mod of h_function); the CRT tail runs in k_decrypt_crt.
+//  key-holder encrypt (ENC = true): x_s = r^n mod s^2 = r^(n mod s(s-1)) mod s^2 (the order
+//    of (Z/s^2)^* is s(s-1)); k_encrypt_crt27 recombines x_p, x_q into r^n mod n^2 -- the
+//    same integer paillier/src/lib.rs:94-98 computes with the public key alone.
+// Output: 32-bit words to Y[tile][2*L1][64] (s = p rows [0,L1), s = q rows [L1, 2L1)).
 // ======================================================================================
-template <int TPI, int W>
-__device__ __forceinline__ void dec_half27(const u32* ctile, u32 col, u32 L32, u32* bcol, u32 qoff,
+template <int TPI, int W, bool ENC>
+__device__ __forceinline__ void pow_half27(const u32* intile, u32 col, u32 inrows, u32* bcol, u32 qoff,
                                            const Tile& tb, const u32* __restrict__ S2, u32 np,
                                            const u32* __restrict__ R1, const u32* __restrict__ R2,
-                                           const u32* __restrict__ sm1, int sm1_bits, int q, L27& A) {
+                                           const u32* __restrict__ ex, int ex_bits, int q, L27& A) {
   constexpr int NL = Geo<TPI>::NL;
   // opaque modulus pointer: keeps LICM from hoisting both halves' limbs (p^2 and q^2) out
   // of the element loop, which would hold 2 x 38 VGPRs for the whole kernel
@@ -189,42 +193,51 @@ __device__ __forceinline__ void dec_half27(const u32* ctile, u32 col, u32 L32, u
   asm volatile("" : "+s"(S2o));
   Mod<TPI> N;
   N.init(S2o, q);
-  // c = c_lo + R c_hi (R = 2^(27 NL)):  X = mont(c_lo, R mod s^2) + mont(c_hi, R^2 mod s^2)
-  // = c mod s^2 up to < 4N (c_lo < R against R1 < N, c_hi tiny); then X R via R^2.
-  L27 B;
-  {
-    const u32 bit0 = 27u * NL + 1026u * q;
-    const ColIO Ci = colio(ctile, L32, col, bit0 >> 5);
-    load_chunk(B, bit0 & 31u, [&](int k) { return Ci.ld(k); });
-  }
-  const_to_slot<TPI>(bcol, qoff, R2, q);
-  mont_mul<TPI>(B, bcol, N, np, q);
-  tab_store(tb, 0, B);  // parked in the (otherwise unused) table entry 0, not in registers
-  {
-    const ColIO Ci = colio(ctile, L32, col, 32u * q);
-    load_chunk(A, 2u * q, [&](int k) { return Ci.ld(k); });
-  }
-  const_to_slot<TPI>(bcol, qoff, R1, q);
-  mont_mul<TPI>(A, bcol, N, np, q);
-  tab_load(B, tb, 0);
+  if constexpr (ENC) {
+    // r < n < 2^(27 NL) = R: one product with R^2 gives r R mod s^2 (< 2N)
+    const ColIO Ri = colio(intile, inrows, col, 32u * q);
+    load_chunk(A, 2u * q, [&](int k) { return Ri.ld(k); });
+    const_to_slot<TPI>(bcol, qoff, R2, q);
+    mont_mul<TPI>(A, bcol, N, np, q);
+  } else {
+    // c = c_lo + R c_hi (R = 2^(27 NL)):  X = mont(c_lo, R mod s^2) + mont(c_hi, R^2 mod s^2)
+    // = c mod s^2 up to < 4N (c_lo < R against R1 < N, c_hi tiny); then X R via R^2.
+    L27 B;
+    {
+      const u32 bit0 = 27u * NL + 1026u * q;
+      const ColIO Ci = colio(intile, inrows, col, bit0 >> 5);
+      load_chunk(B, bit0 & 31u, [&](int k) { return Ci.ld(k); });
+    }
+    const_to_slot<TPI>(bcol, qoff, R2, q);
+    mont_mul<TPI>(B, bcol, N, np, q);
+    tab_store(tb, 0, B);  // parked in the (otherwise unused) table entry 0, not in registers
+    {
+      const ColIO Ci = colio(intile, inrows, col, 32u * q);
+      load_chunk(A, 2u * q, [&](int k) { return Ci.ld(k); });
+    }
+    const_to_slot<TPI>(bcol, qoff, R1, q);
+    mont_mul<TPI>(A, bcol, N, np, q);
+    tab_load(B, tb, 0);
 #pragma unroll
-  for (int j = 0; j < LL; ++j) A.set(j, A[j] + B[j]);
-  normalize_exact<TPI>(A, q);  // < 4N, only ever multiplied by R^2 < N next
-  const_to_slot<TPI>(bcol, qoff, R2, q);
-  mont_mul<TPI>(A, bcol, N, np, q);  // c R, < 2N
-  powm27<TPI, W>(A, bcol, qoff, tb, N, np, sm1, sm1_bits, q);
+    for (int j = 0; j < LL; ++j) A.set(j, A[j] + B[j]);
+    normalize_exact<TPI>(A, q);  // < 4N, only ever multiplied by R^2 < N next
+    const_to_slot<TPI>(bcol, qoff, R2, q);
+    mont_mul<TPI>(A, bcol, N, np, q);  // c R, < 2N
+  }
+  powm27<TPI, W>(A, bcol, qoff, tb, N, np, ex, ex_bits, q);
   one_to_slot<TPI>(bcol, qoff, q);
-  mont_mul<TPI>(A, bcol, N, np, q);  // y = c^(s-1) mod s^2 (< 2N)
+  mont_mul<TPI>(A, bcol, N, np, q);  // leave Montgomery form (< 2N)
   finalize<TPI>(A, N, q);
 }
 
-template <int L, int W>
-__global__ __launch_bounds__(kBlock) void k_decrypt_pow27(KeyArgs K, const u32* __restrict__ C, size_t count,
-                                                          u32* __restrict__ Y, u32* __restrict__ scratch, u32 ldsw) {
+// In: decrypt -- ciphertexts C [T][L][64]; encrypt -- nonces r [T][L/2][64].
+template <int L, int W, bool ENC>
+__global__ __launch_bounds__(kBlock) void k_pow_half27(KeyArgs K, const u32* __restrict__ In, size_t count,
+                                                       u32* __restrict__ Y, u32* __restrict__ scratch, u32 ldsw) {
   constexpr int TPI = L / 64;  // p^2, q^2: 76 limbs for 2048-bit keys, 38 for 1024-bit
   using G = Geo<TPI>;
   constexpr int E = G::E;
-  constexpr u32 L32 = L, L1 = L / 2;
+  constexpr u32 L1 = L / 2, IN = ENC ? L1 : L;
   extern __shared__ __attribute__((aligned(16))) u32 lds[];
   G g;
   const u32 wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -238,19 +251,104 @@ __global__ __launch_bounds__(kBlock) void k_decrypt_pow27(KeyArgs K, const u32* 
     const size_t ebase = (size_t)wt * E;
     const u32 tile = (u32)(ebase >> 6);
     const u32 col = (u32)(ebase & 63) + (u32)g.e;
-    const u32* ctile = C + (size_t)tile * L32 * FPHE_WAVE;
+    const u32* intile = In + (size_t)tile * IN * FPHE_WAVE;
     u32* ytile = Y + (size_t)tile * 2 * L1 * FPHE_WAVE;
     // the two halves in a rolled loop: one inlined copy of the modexp (I-cache)
 #pragma unroll 1
     for (u32 h = 0; h < 2; ++h) {
       const bool hq = h != 0;
+      const u32* ex;
+      int exb;
+      if constexpr (ENC) {
+        ex = hq ? K.eq : K.ep;
+        exb = hq ? K.eq_bits : K.ep_bits;
+      } else {
+        ex = hq ? K.qm1 : K.pm1;
+        exb = hq ? K.qm1_bits : K.pm1_bits;
+      }
       L27 A;
-      dec_half27<TPI, W>(ctile, col, L32, bcol, qoff, tb, hq ? K.Q2_27 : K.P2_27, hq ? K.q2_np27 : K.p2_np27,
-                         hq ? K.Q2R1_27 : K.P2R1_27, hq ? K.Q2R2_27 : K.P2R2_27, hq ? K.qm1 : K.pm1,
-                         hq ? K.qm1_bits : K.pm1_bits, g.q, A);
+      pow_half27<TPI, W, ENC>(intile, col, IN, bcol, qoff, tb, hq ? K.Q2_27 : K.P2_27, hq ? K.q2_np27 : K.p2_np27,
+                              hq ? K.Q2R1_27 : K.P2R1_27, hq ? K.Q2R2_27 : K.P2R2_27, ex, exb, g.q, A);
       const ColIO Yo = colio(ytile, 2 * L1, col, h * L1 + 32u * g.q);
       store_chunk<TPI>(A, g.q, [&](int k, u32 v) { Yo.st(k, v); });
     }
+  }
+}
+
+// ======================================================================================
+// key-holder encrypt, recombination: C = (1 + m n) (x_p Kp + x_q Kq) mod n^2, sign (m < 0)
+// (paillier/src/lib.rs:104-121 with r^n from the CRT halves in Y; bit-identical to the
+// public-key path for the same r).
+// ======================================================================================
+template <int L>
+__global__ __launch_bounds__(kBlock) void k_encrypt_crt27(KeyArgs K, const u32* __restrict__ P, u32 lp,
+                                                          const u8* __restrict__ neg, size_t count,
+                                                          const u32* __restrict__ Y, u32* __restrict__ Cout,
+                                                          u8* __restrict__ sout, u32 ldsw) {
+  constexpr int TPI = L / 32;
+  using G = Geo<TPI>;
+  constexpr int E = G::E;
+  constexpr u32 L32 = L, L1 = L / 2;
+  extern __shared__ __attribute__((aligned(16))) u32 lds[];
+  G g;
+  const u32 wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u32 gw = blockIdx.x * kWavesPerBlock + wib, nw = gridDim.x * kWavesPerBlock;
+  u32* bcol = lds + wib * ldsw * E + g.e;
+  const u32 qoff = lds_qoff<TPI>(g.q);
+  Mod<TPI> N;
+  N.init(K.N2_27, g.q);
+  const u32 np = K.n2_np27;
+  const u32 nwt = (u32)((count + E - 1) / E);
+  for (u32 wt = gw; wt < nwt; wt += nw) {
+    const size_t ebase = (size_t)wt * E;
+    const u32 tile = (u32)(ebase >> 6);
+    const u32 col = (u32)(ebase & 63) + (u32)g.e;
+    const size_t elem = ebase + g.e;
+    const u32* ytile = Y + (size_t)tile * 2 * L1 * FPHE_WAVE;
+    L27 A, B;
+    // x_p Kp + x_q Kq: descriptors of L1 rows each, so words past a half read as 0
+    {
+      const ColIO Xi = colio(ytile, L1, col, 32u * g.q);
+      load_chunk(A, 2u * g.q, [&](int k) { return Xi.ld(k); });
+    }
+    const_to_slot<TPI>(bcol, qoff, K.KpR_27, g.q);
+    mont_mul<TPI>(A, bcol, N, np, g.q);  // x_p Kp (< 2N)
+#pragma unroll
+    for (int k = 0; k < LL / 2; ++k) B.p[k] = A.p[k];
+    {
+      const ColIO Xi = colio(ytile + L1 * FPHE_WAVE, L1, col, 32u * g.q);
+      load_chunk(A, 2u * g.q, [&](int k) { return Xi.ld(k); });
+    }
+    const_to_slot<TPI>(bcol, qoff, K.KqR_27, g.q);
+    mont_mul<TPI>(A, bcol, N, np, g.q);  // x_q Kq (< 2N)
+#pragma unroll
+    for (int j = 0; j < LL; ++j) A.set(j, A[j] + B[j]);
+    normalize_exact<TPI>(A, g.q);        // r^n + k n^2, < 4N, exact limbs
+#pragma unroll
+    for (int k = 0; k < LL / 2; ++k) B.p[k] = A.p[k];
+    // nude ciphertext 1 + m n (32-bit words) into the LDS column, then to 27-bit limbs
+    Tile Pt = make_tile(P + (size_t)tile * lp * FPHE_WAVE, lp * 256u, 0);
+    Pt.vo = col * 4u;
+    bool mneg = false;
+    if (g.q == 0) {
+      mneg = nude_to_slot<L, E>(bcol, K, Pt, lp, neg[elem] != 0);
+      bcol[L * E] = 0;  // the top lane's chunk window reads two words past the number
+      bcol[(L + 1) * E] = 0;
+    }
+    {
+      const u32* src = bcol + 32 * g.q * E;
+      load_chunk(A, 2u * g.q, [&](int k) { return src[k * E]; });
+    }
+    const_to_slot<TPI>(bcol, qoff, K.N2R2_27, g.q);
+    mont_mul<TPI>(A, bcol, N, np, g.q);  // C_nude R (< 2N)
+    to_slot<TPI>(bcol, qoff, A);
+#pragma unroll
+    for (int k = 0; k < LL / 2; ++k) A.p[k] = B.p[k];
+    mont_mul<TPI>(A, bcol, N, np, g.q);  // r^n C_nude (4N x 2N operands: < 2N since R >= 256 N)
+    finalize<TPI>(A, N, g.q);
+    const ColIO Co = colio(Cout + (size_t)tile * L32 * FPHE_WAVE, L32, col, 32u * g.q);
+    store_chunk<TPI>(A, g.q, [&](int k, u32 v) { Co.st(k, v); });
+    if (g.q == 0 && elem < count) sout[elem] = mneg ? 1 : 0;
   }
 }
 

@@ -811,10 +811,18 @@ def _mul(pk: "PK", a: CiphertextVector, p: PlaintextVector, broadcast: bool) -> 
 # keys and coder
 # --------------------------------------------------------------------------------------
 class PK:
-    """``fate_utils.paillier.PK`` (paillier.rs:50-75; fixedpoint_paillier::PK lib.rs:18-34)."""
+    """``fate_utils.paillier.PK`` (paillier.rs:50-75; fixedpoint_paillier::PK lib.rs:18-34).
+
+    A PK made by :func:`keygen` in the process that holds the private key carries a
+    reference to that key's device context (never pickled: ``__getstate__`` is ``n``
+    only, as the reference's).  Its obfuscated encryptions then run the key-holder path
+    (``fphe_encrypt_crt``: r^n mod n^2 from two half-width CRT modexps), which yields the
+    same ciphertext integers as the public-key path for the same r.  ``PK(n)`` -- and any
+    unpickled PK -- is public-only.  ``FPHE_KEYHOLDER_CRT=0`` disables the CRT path."""
 
     def __init__(self, n: Optional[int] = None):
         self.n = n
+        self._priv: Optional[_KeyCtx] = None
         if n is not None:
             self._init(n)
 
@@ -823,6 +831,14 @@ class PK:
         self.ns = n * n
         self.max_int = n // MAX_INT_FRACTION
         self._key = _key_for(n)
+
+    def _bind_private(self, p: int, q: int) -> "PK":
+        self._priv = _key_for(self.n, *((p, q) if p < q else (q, p)))
+        return self
+
+    @property
+    def keyholder(self) -> bool:
+        return self._priv is not None and os.environ.get("FPHE_KEYHOLDER_CRT", "1") != "0"
 
     def encrypt_encoded(self, plaintext_vector: PlaintextVector, obfuscate: bool,
                         r: Optional[Sequence[int]] = None) -> CiphertextVector:
@@ -843,9 +859,16 @@ class PK:
                 raise ValueError("need one r per element")
             rt = torch.from_numpy(rows_to_tiles(ints_to_limbs(list(r), k.L1)).view(np.int32)).to(dev)
         lib = _lib.load()
-        _lib.check(lib.fphe_encrypt(k.ctx(dev), _ptr(pv.P), pv.lp, _ptr(pv.neg), n, 1 if obfuscate else 0,
-                                    _ptr(rt), k.rng_key, k.next_nonce(), _ptr(out.C), _ptr(out.sign),
-                                    ctypes.c_void_p(_stream(dev))), "fphe_encrypt")
+        stream = ctypes.c_void_p(_stream(dev))
+        if obfuscate and self.keyholder:
+            kp = self._priv
+            _lib.check(lib.fphe_encrypt_crt(kp.ctx(dev), _ptr(pv.P), pv.lp, _ptr(pv.neg), n, _ptr(rt), kp.rng_key,
+                                            kp.next_nonce(), _ptr(out.C), _ptr(out.sign), stream),
+                       "fphe_encrypt_crt")
+        else:
+            _lib.check(lib.fphe_encrypt(k.ctx(dev), _ptr(pv.P), pv.lp, _ptr(pv.neg), n, 1 if obfuscate else 0,
+                                        _ptr(rt), k.rng_key, k.next_nonce(), _ptr(out.C), _ptr(out.sign), stream),
+                       "fphe_encrypt")
         out.exp[:n] = pv.exp[:n]
         return out
 
@@ -857,6 +880,7 @@ class PK:
         return {"n": self.n}
 
     def __setstate__(self, st):
+        self._priv = None
         self._init(st["n"])
 
 
@@ -1115,9 +1139,13 @@ class Evaluator:
 def keygen(bit_length: int) -> Tuple[SK, PK, Coder]:
     """``fate_utils.paillier.keygen`` (paillier.rs:206-210; fixedpoint_paillier::keygen lib.rs:408-413)."""
     p, q = keygen_primes(bit_length)
-    return SK(p, q), PK(p * q), Coder(p * q)
+    return SK(p, q), PK(p * q)._bind_private(p, q), Coder(p * q)
 
 
-def keypair_from_primes(p: int, q: int) -> Tuple[SK, PK, Coder]:
-    """Deterministic key construction for tests / fixtures."""
-    return SK(p, q), PK(p * q), Coder(p * q)
+def keypair_from_primes(p: int, q: int, keyholder: bool = True) -> Tuple[SK, PK, Coder]:
+    """Deterministic key construction for tests / fixtures.  ``keyholder=False`` gives a
+    public-only PK (the encrypting party without the private key)."""
+    pk = PK(p * q)
+    if keyholder:
+        pk._bind_private(p, q)
+    return SK(p, q), pk, Coder(p * q)

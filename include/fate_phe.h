@@ -124,6 +124,18 @@ fphe_status fphe_encrypt(fphe_ctx* ctx, const uint32_t* P, uint32_t lp, const ui
                          const uint32_t rng_key[8], uint64_t rng_nonce,
                          uint32_t* C, uint8_t* sign, void* stream);
 
+/* Key-holder obfuscated encryption (extension; same output as fphe_encrypt with
+ * obfuscate=1 for the same r).  The reference computes r^n mod n^2 with the public key
+ * alone (crates/paillier/src/lib.rs:94-98, 116); with p, q resident the same integer is
+ * the CRT recombination of r^(n mod p(p-1)) mod p^2 and r^(n mod q(q-1)) mod q^2, two
+ * half-width modexps (about half the multiply work).  FATE's encrypting parties
+ * (Hetero-LR / SecureBoost guest, arch/context/_cipher.py) hold the private key they
+ * generated.  Requires a context created with p, q (else FPHE_ERR_NO_SK); r and rng_*
+ * as fphe_encrypt. */
+fphe_status fphe_encrypt_crt(fphe_ctx* ctx, const uint32_t* P, uint32_t lp, const uint8_t* neg,
+                             size_t count, const uint32_t* r, const uint32_t rng_key[8],
+                             uint64_t rng_nonce, uint32_t* C, uint8_t* sign, void* stream);
+
 /* Decrypt to encoded plaintext: SK.decrypt_to_encoded (paillier.rs:79-81) ->
  * paillier::SK::decrypt (crates/paillier/src/lib.rs:163-176), CRT.
  * Output P[T][L1][64] in [0, n). */

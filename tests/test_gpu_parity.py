@@ -51,8 +51,14 @@ def test_encode_f32(fx):
     assert exp == f["encrypt"]["exp"]
 
 
-def test_encrypt_injected_r(fx):
+@pytest.mark.parametrize("keyholder", [False, True], ids=["public", "keyholder_crt"])
+def test_encrypt_injected_r(fx, keyholder):
+    """Public-key path (fphe_encrypt) and key-holder CRT path (fphe_encrypt_crt): both must
+    give the reference's ciphertext integers for the same r."""
     f, sk, pk, coder = fx
+    if not keyholder:
+        pk = P.PK(pk.n)
+    assert pk.keyholder == keyholder
     e = f["encrypt"]
     pv = P.PlaintextVector.from_ints([int(s, 16) for s in e["sig"]], e["exp"])
     ct = pk.encrypt_encoded(pv, True, r=[int(r, 16) for r in e["r"]])
@@ -96,9 +102,12 @@ def test_mul(fx):
     assert ct_list(pk, c.mul(pk, pv)) == [[x, e] for x, e in f["mul"]["out"]]
 
 
-def test_roundtrip_device_rng(fx):
+@pytest.mark.parametrize("keyholder", [False, True], ids=["public", "keyholder_crt"])
+def test_roundtrip_device_rng(fx, keyholder):
     """decrypt(encrypt(x)) == x with device-drawn r (reference test crates/paillier/src/lib.rs:190-197)."""
     f, sk, pk, coder = fx
+    if not keyholder:
+        pk = P.PK(pk.n)
     x = torch.tensor(f["encrypt"]["x_f32"], dtype=torch.float32).cuda()
     ct = pk.encrypt_encoded(coder.encode_f32_vec(x), True)
     y = coder.decode_f32_vec(sk.decrypt_to_encoded(ct))
