@@ -7,6 +7,10 @@
 #include "mont27_dev.h"
 #include "inv27.h"
 
+// Montgomery-engine kernels target 2 waves per SIMD (<= 256 VGPRs, no AGPR overflow): the
+// v_mad_u64_u32 stream needs two waves to issue at full rate.
+#define FPHE_OCC2 __attribute__((amdgpu_waves_per_eu(2)))
+
 namespace {
 
 using namespace fphe::r27;
@@ -113,7 +117,7 @@ __device__ __forceinline__ void powm27(L27& A, u32* bcol, u32 qoff, const Tile& 
 // encrypt (27-bit engine): TPI = 4 for 2048-bit keys (n^2: 152 limbs), 2 for 1024-bit.
 // ======================================================================================
 template <int L, int W>
-__global__ __launch_bounds__(kBlock) void k_encrypt27(KeyArgs K, const u32* __restrict__ P, u32 lp,
+__global__ __launch_bounds__(kBlock) FPHE_OCC2 void k_encrypt27(KeyArgs K, const u32* __restrict__ P, u32 lp,
                                                       const u8* __restrict__ neg, size_t count, int obf,
                                                       const u32* __restrict__ rin, u32* __restrict__ Cout,
                                                       u8* __restrict__ sout, u32* __restrict__ scratch, u32 ldsw) {
@@ -232,7 +236,7 @@ __device__ __forceinline__ void pow_half27(const u32* intile, u32 col, u32 inrow
 
 // In: decrypt -- ciphertexts C [T][L][64]; encrypt -- nonces r [T][L/2][64].
 template <int L, int W, bool ENC>
-__global__ __launch_bounds__(kBlock) void k_pow_half27(KeyArgs K, const u32* __restrict__ In, size_t count,
+__global__ __launch_bounds__(kBlock) FPHE_OCC2 void k_pow_half27(KeyArgs K, const u32* __restrict__ In, size_t count,
                                                        u32* __restrict__ Y, u32* __restrict__ scratch, u32 ldsw) {
   constexpr int TPI = L / 64;  // p^2, q^2: 76 limbs for 2048-bit keys, 38 for 1024-bit
   using G = Geo<TPI>;
@@ -281,7 +285,7 @@ __global__ __launch_bounds__(kBlock) void k_pow_half27(KeyArgs K, const u32* __r
 // public-key path for the same r).
 // ======================================================================================
 template <int L>
-__global__ __launch_bounds__(kBlock) void k_encrypt_crt27(KeyArgs K, const u32* __restrict__ P, u32 lp,
+__global__ __launch_bounds__(kBlock) FPHE_OCC2 void k_encrypt_crt27(KeyArgs K, const u32* __restrict__ P, u32 lp,
                                                           const u8* __restrict__ neg, size_t count,
                                                           const u32* __restrict__ Y, u32* __restrict__ Cout,
                                                           u8* __restrict__ sout, u32 ldsw) {
@@ -356,7 +360,7 @@ __global__ __launch_bounds__(kBlock) void k_encrypt_crt27(KeyArgs K, const u32* 
 // ct-add (fixedpoint_paillier/src/lib.rs:301-333), 27-bit engine
 // ======================================================================================
 template <int L>
-__global__ __launch_bounds__(kBlock) void k_add27(KeyArgs K, const u32* __restrict__ Ca, const u8* __restrict__ sa,
+__global__ __launch_bounds__(kBlock) FPHE_OCC2 void k_add27(KeyArgs K, const u32* __restrict__ Ca, const u8* __restrict__ sa,
                                                   const int32_t* __restrict__ ea, const u32* __restrict__ Cb,
                                                   const u8* __restrict__ sb, const int32_t* __restrict__ eb,
                                                   int bstride, size_t count, u32* __restrict__ Co,
@@ -517,7 +521,7 @@ __global__ __launch_bounds__(256) void k_mul_prep(KeyArgs K, const u32* __restri
 
 // ======================================================================================
 template <int L, int W>
-__global__ __launch_bounds__(kBlock) void k_mul27(KeyArgs K, const u32* __restrict__ Ca, const u32* __restrict__ Cinv,
+__global__ __launch_bounds__(kBlock) FPHE_OCC2 void k_mul27(KeyArgs K, const u32* __restrict__ Ca, const u32* __restrict__ Cinv,
                                                   const u8* __restrict__ need, const int32_t* __restrict__ ea,
                                                   const u32* __restrict__ Ex, const int32_t* __restrict__ ebits_in,
                                                   const int32_t* __restrict__ pexp, int pstride, size_t count,
@@ -613,7 +617,7 @@ __global__ __launch_bounds__(kBlock) void k_mul27(KeyArgs K, const u32* __restri
 // result * y % ns; the powm result is canonical, so the product's sign is y's).
 // ======================================================================================
 template <int L>
-__global__ __launch_bounds__(kBlock) void k_sqmul27(KeyArgs K, const u32* __restrict__ Ca, const u32* __restrict__ Cb,
+__global__ __launch_bounds__(kBlock) FPHE_OCC2 void k_sqmul27(KeyArgs K, const u32* __restrict__ Ca, const u32* __restrict__ Cb,
                                                     const u8* __restrict__ sb, int nsq, size_t count,
                                                     u32* __restrict__ Co, u8* __restrict__ so, u32 ldsw) {
   constexpr int TPI = L / 32;
@@ -716,7 +720,7 @@ __global__ __launch_bounds__(kBlock) void k_inv_n27(KeyArgs K, const u32* __rest
 }
 
 template <int L>
-__global__ __launch_bounds__(kBlock) void k_inv_lift27(KeyArgs K, const u32* __restrict__ C, size_t count,
+__global__ __launch_bounds__(kBlock) FPHE_OCC2 void k_inv_lift27(KeyArgs K, const u32* __restrict__ C, size_t count,
                                                        const u8* __restrict__ need, const u32* __restrict__ X0,
                                                        u32* __restrict__ Co, u32 ldsw) {
   constexpr int TPI = L / 32;

@@ -158,18 +158,22 @@ __device__ __forceinline__ void normalize_almost(const u64 (&T)[LL], L27& A, int
 }
 
 // One reduction row: m = T_0 n' mod 2^27 (broadcast from the element's lane 0), then
-// T = (T + m N) / 2^27 with the word leaving each lane's bottom limb passed to the top limb
-// of the lane below.
+// T = (T + m N) / 2^27.  The word X leaving a lane's bottom limb (old position 38q) lands
+// at new position 38q - 1, i.e. X 2^(27(38q-1)) = (X >> 27) 2^(27 38q) + (X mod 2^27)
+// 2^(27(38q-1)): its high part stays in the lane's own new bottom limb and only the low 27
+// bits move to the top limb of the lane below.  Lane 0's X is 0 mod 2^27 (the point of m),
+// so what the previous element's top lane receives from it is 0, as required: no lane
+// selects at all.
 template <int TPI>
 __device__ __forceinline__ void red_row(u64 (&T)[LL], const Mod<TPI>& N, const u32 nprime, int q) {
+  (void)q;
   const u32 m = dpp_bcast<TPI>(((u32)T[0] * nprime) & MASK);
   // X = m N_0 + T_0 ; T_{j-1} = m N_j + T_j  (the shift by one limb)
   u64 X;
   if constexpr (TPI > 1) {
     asm volatile(R27_ASM_REDROW : [x] "=&v"(X), R27_T_OPS(T) : [m] "v"(m), R27_N_INS(N, "v") : "vcc", "memory");
-    T[0] += (q == 0) ? (X >> LB) : 0ull;  // lowest limb: X = 0 mod 2^27
-    const u64 up = dpp_from_next64(X);     // X of the lane above
-    T[LL - 1] = (q == TPI - 1) ? 0ull : up;
+    T[0] += X >> LB;
+    T[LL - 1] = dpp_from_next64(X & (u64)MASK);  // row end (lane 15): 0, a top lane anyway
   } else {
     asm volatile(R27_ASM_REDROW : [x] "=&v"(X), R27_T_OPS(T) : [m] "v"(m), R27_N_INS(N, "s") : "vcc", "memory");
     T[0] += X >> LB;
