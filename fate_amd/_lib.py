@@ -33,6 +33,7 @@ EXPORTED_SYMBOLS = (
     "fphe_encode_f32", "fphe_encode_f64", "fphe_decode_f32", "fphe_decode_f64",
     "fphe_encode_i64", "fphe_decode_i64", "fphe_decode_i32", "fphe_pack_f64", "fphe_unpack_f64",
     "fphe_encrypt", "fphe_encrypt_crt", "fphe_decrypt", "fphe_add", "fphe_mul", "fphe_neg", "fphe_sqmul",
+    "fphe_fold",
 )
 
 _lock = threading.Lock()
@@ -100,6 +101,8 @@ def load() -> ctypes.CDLL:
         lib.fphe_neg.restype = st
         lib.fphe_sqmul.argtypes = [vp, vp, vp, vp, ctypes.c_uint32, ctypes.c_size_t, vp, vp, vp]
         lib.fphe_sqmul.restype = st
+        lib.fphe_fold.argtypes = [vp, vp, vp, vp, vp, vp, vp, ctypes.c_size_t, vp, vp, vp, vp]
+        lib.fphe_fold.restype = st
         _lib = lib
         return lib
 

@@ -57,6 +57,7 @@ struct KeyArgs {
   const u32* ep; const u32* eq;          // n mod p(p-1), n mod q(q-1)           [L1]
   int ep_bits, eq_bits;
   const u32* KpR_27; const u32* KqR_27;  // Kp R, Kq R mod n^2 (27-bit, R = 2^(27 NL2)) [NL2]
+  const u32* FR_27;                      // R^k mod n^2, k = 0..kFoldMax               [kFoldMax+1][NL2]
 };
 
 __device__ __forceinline__ void set_err(int32_t* err, u32 f) {
@@ -1066,6 +1067,20 @@ fphe_status launch_encrypt_crt27(fphe_ctx* c, const uint32_t* P, uint32_t lp, co
 }
 
 template <int L>
+fphe_status launch_fold27(fphe_ctx* c, const uint32_t* Src, const uint8_t* ssign, const int32_t* sexp,
+                          const int64_t* ord, const int64_t* cstart, const int32_t* clen, size_t nchunks,
+                          uint32_t* Co, uint8_t* so, int32_t* eo, hipStream_t s) {
+  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = r27::LL * TPI;
+  auto kern = k_fold27<L>;
+  const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
+  set_lds(kern, lds);
+  const unsigned grid = occ_grid(c, kern, lds, (nchunks + E - 1) / E, "fold27");
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, Src, ssign, sexp, ord, cstart, clen, nchunks,
+                     c->K.FR_27, Co, so, eo, (u32)NL);
+  return hip_ok(hipGetLastError());
+}
+
+template <int L>
 fphe_status launch_add27(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, const int32_t* ea, const uint32_t* Cb,
                          const uint8_t* sb, const int32_t* eb, int bstride, size_t count, uint32_t* Co, uint8_t* so,
                          int32_t* eo, hipStream_t s) {
@@ -1181,6 +1196,17 @@ fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, 
     const size_t o_N2_27 = put(to27(N2, NL2), NL2);
     const size_t o_N2R1_27 = put(to27(hbn::pow2_mod((size_t)27 * NL2, N2), NL2), NL2);
     const size_t o_N2R2_27 = put(to27(hbn::pow2_mod((size_t)54 * NL2, N2), NL2), NL2);
+    // R^k mod n^2, k = 0..kFoldMax (27-bit limbs): the k_fold27 fix-up factors
+    size_t o_FR = 0;
+    {
+      const Limbs R27 = hbn::pow2_mod((size_t)27 * NL2, N2);
+      Limbs x{1};
+      for (int k = 0; k <= kFoldMax; ++k) {
+        const size_t o = put(to27(x, NL2), NL2);
+        if (k == 0) o_FR = o;
+        x = hbn::mod(hbn::mul(x, R27), N2);
+      }
+    }
     const size_t o_Nn_27 = put(to27(n, NLh), NLh);
     const size_t o_NnR1_27 = put(to27(hbn::pow2_mod((size_t)27 * NLh, n), NLh), NLh);
     const size_t o_NnR2_27 = put(to27(hbn::pow2_mod((size_t)54 * NLh, n), NLh), NLh);
@@ -1258,6 +1284,7 @@ fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, 
     K.nbits = (int)key_bits;
     K.N2_27 = b + o_N2_27; K.N2R1_27 = b + o_N2R1_27; K.N2R2_27 = b + o_N2R2_27;
     K.n2_np27 = K.n2_n0inv & ((1u << 27) - 1u);
+    K.FR_27 = b + o_FR;
     K.Nn_27 = b + o_Nn_27; K.NnR1_27 = b + o_NnR1_27; K.NnR2_27 = b + o_NnR2_27;
     K.nn_np27 = hbn::neg_inv32(n[0]) & ((1u << 27) - 1u);
     K.nn_inv27 = (0u - hbn::neg_inv32(n[0])) & ((1u << 27) - 1u);
@@ -1463,6 +1490,21 @@ fphe_status fphe_encrypt_crt(fphe_ctx* c, const uint32_t* P, uint32_t lp, const 
   if (c->L2 == 128)
     return launch_encrypt_crt27<128>(c, P, lp, neg, count, r, rng_key, nonce, C, sign, (hipStream_t)stream);
   return launch_encrypt_crt27<64>(c, P, lp, neg, count, r, rng_key, nonce, C, sign, (hipStream_t)stream);
+}
+
+
+fphe_status fphe_fold(fphe_ctx* c, const uint32_t* Src, const uint8_t* ssign, const int32_t* sexp,
+                      const int64_t* ord, const int64_t* cstart, const int32_t* clen, size_t nchunks,
+                      uint32_t* Co, uint8_t* so, int32_t* eo, void* stream) {
+  if (!c) return FPHE_ERR_ARG;
+  if (nchunks == 0) return FPHE_OK;
+  if (!Src || !ssign || !sexp || !ord || !cstart || !clen || !Co || !so || !eo) return FPHE_ERR_ARG;
+  if (nchunks >= (1ull << 32)) return FPHE_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DevGuard g(c->device);
+  if (c->L2 == 128)
+    return launch_fold27<128>(c, Src, ssign, sexp, ord, cstart, clen, nchunks, Co, so, eo, (hipStream_t)stream);
+  return launch_fold27<64>(c, Src, ssign, sexp, ord, cstart, clen, nchunks, Co, so, eo, (hipStream_t)stream);
 }
 
 

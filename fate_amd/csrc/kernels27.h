@@ -612,6 +612,102 @@ __global__ __launch_bounds__(kBlock) FPHE_OCC2 void k_mul27(KeyArgs K, const u32
 }
 
 // ======================================================================================
+// Segmented product fold: the ciphertext-add fold of same-exponent terms, one chunk of up
+// to kFoldMax consecutive terms of a sorted index list per element, in one pass.
+// For terms with equal exponents Ciphertext::add (fixedpoint_paillier/src/lib.rs:301-333)
+// is the product mod n^2 with the signs XOR-ed (no alignment), and the literal-1 rule is
+// the identity of that product, so a chunk is folded as
+//   acc = t_0; acc = mont(acc, t_j) for j >= 1  (= prod t . R^-(len-1)); acc = mont(acc, R^len)
+// -- one Montgomery product per term, terms read straight from the source vector by index
+// (no gather copies).  The callers (iupdate, intervals_sum, matmul folds) group terms by
+// (segment, exponent) so every chunk is single-exponent; the few per-exponent partials of a
+// segment are then merged with the aligning ct-add (k_add27).  Bit-exact by the order
+// independence of the fold.
+// ======================================================================================
+constexpr int kFoldMax = 64;
+
+template <int L>
+__global__ __launch_bounds__(kBlock) FPHE_OCC2 void k_fold27(KeyArgs K, const u32* __restrict__ Src,
+                                                             const u8* __restrict__ ssign,
+                                                             const int32_t* __restrict__ sexp,
+                                                             const int64_t* __restrict__ ord,
+                                                             const int64_t* __restrict__ cstart,
+                                                             const int32_t* __restrict__ clen, size_t nchunks,
+                                                             const u32* __restrict__ FR, u32* __restrict__ Co,
+                                                             u8* __restrict__ so, int32_t* __restrict__ eo, u32 ldsw) {
+  constexpr int TPI = L / 32;
+  using G = Geo<TPI>;
+  constexpr int E = G::E, NL = G::NL;
+  constexpr u32 L32 = L;
+  extern __shared__ __attribute__((aligned(16))) u32 lds[];
+  G g;
+  const u32 wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u32 gw = blockIdx.x * kWavesPerBlock + wib, nw = gridDim.x * kWavesPerBlock;
+  u32* bcol = lds + wib * ldsw * E + g.e;
+  const u32 qoff = lds_qoff<TPI>(g.q);
+  Mod<TPI> N;
+  N.init(K.N2_27, g.q);
+  const u32 np = K.n2_np27;
+  // the 34 words of this lane's 1026-bit chunk of source element `idx` (0 past the number)
+  auto fetch = [&](int64_t idx, u32 (&W)[34]) {
+    const u32* base = Src + ((size_t)(idx >> 6) * L32 * FPHE_WAVE + (size_t)(idx & 63)) + (size_t)32 * g.q * FPHE_WAVE;
+#pragma unroll
+    for (int k = 0; k < 34; ++k) W[k] = (32 * g.q + k < (int)L32) ? base[(size_t)k * FPHE_WAVE] : 0u;
+  };
+  const u32 nwt = (u32)((nchunks + E - 1) / E);
+  for (u32 wt = gw; wt < nwt; wt += nw) {
+    const size_t ebase = (size_t)wt * E;
+    const u32 tile = (u32)(ebase >> 6);
+    const u32 col = (u32)(ebase & 63) + (u32)g.e;
+    const size_t ch = ebase + g.e;
+    const bool inside = ch < nchunks;
+    const int64_t st = inside ? cstart[ch] : 0;
+    const int len = inside ? clen[ch] : 0;
+    const int maxlen = wave_max_int(len);
+    L27 A, B;
+    u32 W[34];
+    u32 sg = 0;
+    int ex = 0;
+    if (inside) {
+      const int64_t i0 = ord[st];
+      fetch(i0, W);
+      sg = ssign[i0];
+      ex = sexp[i0];
+    } else {
+#pragma unroll
+      for (int k = 0; k < 34; ++k) W[k] = 0;
+    }
+    load_chunk(A, 2u * g.q, [&](int k) { return W[k]; });
+    if (len > 1) fetch(ord[st + 1], W);
+    // term j's words are fetched during product j-1 (software pipelined gathers)
+#pragma unroll 1
+    for (int j = 1; j < maxlen; ++j) {
+      if (j < len) {
+        load_chunk(B, 2u * g.q, [&](int k) { return W[k]; });
+        sg ^= ssign[ord[st + j]];
+        to_slot<TPI>(bcol, qoff, B);
+        if (j + 1 < len) fetch(ord[st + j + 1], W);
+        mont_mul<TPI>(A, bcol, N, np, g.q);
+      }
+    }
+    // undo the R^-(len-1): one product with R^len mod n^2 (FR row len)
+    {
+      const u32* f = FR + (size_t)(len > 0 ? len : 1) * NL + g.q * LL;
+#pragma unroll
+      for (int j = 0; j < LL; ++j) bcol[qoff + j * E] = f[j];
+    }
+    mont_mul<TPI>(A, bcol, N, np, g.q);
+    finalize<TPI>(A, N, g.q);
+    const ColIO Oo = colio(Co + (size_t)tile * L32 * FPHE_WAVE, L32, col, 32u * g.q);
+    store_chunk<TPI>(A, g.q, [&](int k, u32 v) { Oo.st(k, v); });
+    if (g.q == 0 && inside) {
+      so[ch] = (u8)sg;
+      eo[ch] = ex;
+    }
+  }
+}
+
+// ======================================================================================
 // Co = Ca^(2^nsq) * Cb mod n^2, sign = sign(b): one step of pack_squeeze
 // (fixedpoint_paillier/src/lib.rs:439-450: result.pow_mod_mut(2^shift) then
 // result * y % ns; the powm result is canonical, so the product's sign is y's).

@@ -568,17 +568,22 @@ class CiphertextVector:
 
     def _scatter_fold(self, other: "CiphertextVector", ii: torch.Tensor, pp: torch.Tensor, stride: int,
                       pk: "PK") -> None:
+        """data[pp*stride+t] += other[ii*stride+t] for all listed pairs, in the reference's
+        order (sample-major).  The terms are folded per slot straight out of ``other``
+        (fphe_fold reads them by index), then added to the slot's current value:
+        fold(data[s], t_1, ..., t_k) = add(data[s], fold(t_1, ..., t_k)), literal-1 rule
+        included."""
         if ii.numel() == 0:
             return
-        t = torch.arange(stride)
+        dev = self.device
+        ii, pp = ii.to(dev), pp.to(dev)
+        t = torch.arange(stride, device=dev)
         src = (ii[:, None] * stride + t).reshape(-1)
         slot = (pp[:, None] * stride + t).reshape(-1)
         if int(slot.max()) >= self.count or int(src.max()) >= other.count:
             raise PanicException("index out of bounds")
-        uniq = torch.unique(slot)
-        terms = Evaluator.cat([self._gather(uniq), other._gather(src)])
-        folded, ids = _fold_segments(pk, terms, torch.cat([uniq, slot]))
-        self._assign(ids, folded)
+        folded, ids = _fold_segments(pk, other, slot, index=src)
+        self._assign(ids, _add(pk, self._gather(ids), folded, broadcast=False))
 
     def chunking_cumsum_with_step(self, pk: "PK", chunk_sizes: Sequence[int], step: int) -> None:
         """``CiphertextVector::chunking_cumsum_with_step`` (lib.rs:760-771): within each chunk,
@@ -617,7 +622,7 @@ class CiphertextVector:
         if idx:
             ia, sa_ = torch.cat(idx), torch.cat(seg)
             if ia.numel():
-                folded, ids = _fold_segments(pk, self._gather(ia), sa_)
+                folded, ids = _fold_segments(pk, self, sa_, index=ia)
                 out._assign(ids, folded)
         return out
 
@@ -705,7 +710,79 @@ def _flatten_positions(indexes) -> Tuple[torch.Tensor, torch.Tensor]:
     return ii, pp
 
 
-def _fold_segments(pk: "PK", src: CiphertextVector, seg: torch.Tensor) -> Tuple[CiphertextVector, torch.Tensor]:
+FOLD_MAX = 64  # terms per chunk of fphe_fold (kFoldMax in kernels27.h)
+
+
+def _run_starts(head: torch.Tensor) -> torch.Tensor:
+    """For run-head flags, the index of each position's run start (a cumsum and a gather;
+    cheaper on the device than cummax-with-indices)."""
+    heads = torch.nonzero(head).squeeze(1)
+    return heads[torch.cumsum(head.to(torch.int32), 0) - 1]
+
+
+def _fold_chunks(pk: "PK", src: CiphertextVector, ordv: torch.Tensor, keys: torch.Tensor
+                 ) -> Tuple[CiphertextVector, torch.Tensor]:
+    """One fphe_fold pass: the terms src[ordv[i]] carry sorted group keys keys[i]; every run of
+    equal keys is cut into chunks of <= FOLD_MAX terms and each chunk becomes one partial.
+    Returns the partials (in key order) and their keys."""
+    dev = src.device
+    n = keys.numel()
+    pos = torch.arange(n, device=dev)
+    head = torch.ones(n, dtype=torch.bool, device=dev)
+    head[1:] = keys[1:] != keys[:-1]
+    gstart = _run_starts(head)
+    cstart = torch.nonzero(head | ((pos - gstart) % FOLD_MAX == 0)).squeeze(1)
+    nch = cstart.numel()
+    clen = torch.diff(cstart, append=torch.tensor([n], device=dev)).to(torch.int32)
+    out = CiphertextVector.empty(nch, pk._key.L2, dev)
+    lib = _lib.load()
+    _lib.check(lib.fphe_fold(pk._key.ctx(dev), _ptr(src.C), _ptr(src.sign), _ptr(src.exp),
+                             _ptr(ordv.to(torch.int64).contiguous()), _ptr(cstart.contiguous()), _ptr(clen), nch,
+                             _ptr(out.C), _ptr(out.sign), _ptr(out.exp), ctypes.c_void_p(_stream(dev))), "fphe_fold")
+    return out, keys[cstart]
+
+
+def _fold_segments(pk: "PK", src: CiphertextVector, seg: torch.Tensor, index: Optional[torch.Tensor] = None
+                   ) -> Tuple[CiphertextVector, torch.Tensor]:
+    """Fold the terms src[index[i]] (index defaults to all of src) by segment id seg[i]: the
+    reference's sequential ct-add folds, which are order-independent.
+    Terms are sorted by (segment, exponent): equal-exponent runs are folded as plain
+    products by fphe_fold (chunks of 64, repeated until one partial per (segment,
+    exponent)), then each segment's per-exponent partials are merged by the aligning ct-add
+    tree.  Returns one ciphertext per non-empty segment with the segment ids (ascending)."""
+    dev = src.device
+    src = _fit_limbs(src, pk._key.L2)
+    seg = seg.to(dev, torch.long)
+    n = seg.numel()
+    if n == 0:
+        return CiphertextVector.empty(0, pk._key.L2, dev), seg
+    index = torch.arange(n, device=dev) if index is None else index.to(dev, torch.long)
+    texp = src.exp[index]
+    key = seg * (1 << 32) + (texp.to(torch.long) + (1 << 31))
+    key, order = torch.sort(key)
+    cur, ckeys = _fold_chunks(pk, src, index[order], key)
+    while bool((ckeys[1:] == ckeys[:-1]).any()):
+        cur, ckeys = _fold_chunks(pk, cur, torch.arange(cur.count, device=dev), ckeys)
+    res, ids = _fold_tree(pk, cur, ckeys >> 32)
+    # A segment whose terms are all the literal 1 folds to 1: add(1, y) returns y, so the
+    # reference's sequential fold ends on its LAST term, exponent included (lib.rs:303-308).
+    lit = _is_literal_one(res)
+    if bool(lit.any()):
+        pos = torch.arange(n, device=dev)
+        last = torch.zeros(int(seg.max()) + 1, dtype=torch.long, device=dev)
+        last.scatter_reduce_(0, seg, pos, reduce="amax", include_self=False)
+        li = torch.nonzero(lit).squeeze(1)
+        res.exp[li] = texp[last[ids[li]]]
+    return res, ids
+
+
+def _is_literal_one(v: CiphertextVector) -> torch.Tensor:
+    """Per element: is the signed ciphertext integer exactly 1 (the reference's zero)."""
+    rows = gather_rows(v.C, torch.arange(v.count, device=v.device))
+    return (rows[:, 0] == 1) & (rows[:, 1:] == 0).all(dim=1) & (v.sign[: v.count] == 0)
+
+
+def _fold_tree(pk: "PK", src: CiphertextVector, seg: torch.Tensor) -> Tuple[CiphertextVector, torch.Tensor]:
     """Fold src by segment id with the ct-add kernel, as a pairwise tree inside each
     segment (ceil(log2(longest segment)) launches).  Returns one folded ciphertext per
     non-empty segment, with the segment ids (ascending)."""
@@ -719,7 +796,7 @@ def _fold_segments(pk: "PK", src: CiphertextVector, seg: torch.Tensor) -> Tuple[
         pos = torch.arange(n, device=dev)
         head = torch.ones(n, dtype=torch.bool, device=dev)
         head[1:] = ids[1:] != ids[:-1]
-        start = torch.cummax(torch.where(head, pos, torch.zeros_like(pos)), 0).values
+        start = _run_starts(head)
         left = pos[(pos - start) % 2 == 0]
         nxt = torch.clamp(left + 1, max=n - 1)
         has = (left + 1 < n) & (ids[nxt] == ids[left])
@@ -742,12 +819,9 @@ def _matmul_terms(pk: "PK", a: CiphertextVector, b: PlaintextVector, ai: torch.T
     for s0 in range(0, ai.numel(), chunk):
         sl = slice(s0, s0 + chunk)
         prod = _mul(pk, a._gather(ai[sl]), b._gather(bi[sl].to(b.device)), broadcast=False)
-        seg = oi[sl]
-        if s0:  # fold the running partial sums in with this chunk's terms
-            touched = torch.unique(seg)
-            prod = Evaluator.cat([out._gather(touched), prod])
-            seg = torch.cat([touched, seg])
-        folded, ids = _fold_segments(pk, prod, seg)
+        folded, ids = _fold_segments(pk, prod, oi[sl])
+        if s0:  # the running partial sums come first: fold(out, terms) = add(out, fold(terms))
+            folded = _add(pk, out._gather(ids), folded, broadcast=False)
         out._assign(ids, folded)
     return out
 

@@ -164,6 +164,19 @@ fphe_status fphe_mul(fphe_ctx* ctx, const uint32_t* Ca, const uint8_t* sa, const
 fphe_status fphe_neg(fphe_ctx* ctx, const uint32_t* C, size_t count, uint32_t* Co, int32_t* err,
                      void* stream);
 
+/* Segmented same-exponent fold (the ct-add fold inside CiphertextVector.iupdate /
+ * iupdate_with_masks / intervals_sum_with_step / matmul, paillier.rs:300-340, 378-386;
+ * fixedpoint_paillier/src/lib.rs:724-791, 861-908, Ciphertext::add :301-333): chunk i
+ * folds the terms Src[ord[cstart[i] + j]], j < clen[i] (1 <= clen[i] <= 64), into
+ * Co[i] = prod C mod n^2, so[i] = XOR of signs, eo[i] = the exponent of the chunk's
+ * first term.  The caller groups terms by (segment, exponent): for equal exponents the
+ * reference's add is exactly this product (literal 1 is its identity), and the
+ * per-exponent partials are merged with fphe_add.  ord / cstart are int64 element
+ * indexes, clen int32; Co is [ceil(nchunks/64)][L2][64]. */
+fphe_status fphe_fold(fphe_ctx* ctx, const uint32_t* Src, const uint8_t* ssign, const int32_t* sexp,
+                      const int64_t* ord, const int64_t* cstart, const int32_t* clen, size_t nchunks,
+                      uint32_t* Co, uint8_t* so, int32_t* eo, void* stream);
+
 /* Co = Ca^(2^nsq) * Cb mod n^2 with so = sb: the step of CiphertextVector::pack_squeeze
  * (paillier.rs:241-243; fixedpoint_paillier/src/lib.rs:439-450), `result.pow_mod_mut(2^shift)`
  * then `result * y % ns` (the powm result is canonical, so the product takes y's sign). */

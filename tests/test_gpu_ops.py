@@ -146,6 +146,41 @@ def test_iupdate_and_masks(env1024):
     assert host(pk, v2) == ref(want2)
 
 
+def _fold_terms(opk, count, seed):
+    """Terms for the segmented fold: long equal-exponent runs (> 64, several fphe_fold
+    rounds), negative significands (sign 1), other exponents, literal 1s with exponent 0
+    and -14 (the nude encryption of 0.0 is the integer 1, which add() treats as zero)."""
+    rng = random.Random(seed)
+    terms = []
+    for i in range(count):
+        exp = rng.choice([0, 0, 0, 0, -3, 2, -1])
+        sig = rng.randrange(1, 1 << 40) * rng.choice([1, -1])
+        pt = O.Plaintext(sig if sig >= 0 else sig, exp)
+        terms.append(O.fp_encrypt(opk, pt, True, 1 + rng.randrange(opk.n - 1)))
+    terms[5] = O.fp_encrypt(opk, O.encode_f64(opk.n, 0.0), False)  # integer 1, exp -14
+    terms[9] = O.ct_zero()
+    return terms
+
+
+def test_iupdate_long_segments(env1024):
+    """iupdate with hundreds of terms per slot: exercises fphe_fold's multi-round chunking
+    and the per-exponent merge against the reference's sequential fold."""
+    fx, sk, pk, coder, opk, cts = env1024
+    rng = random.Random(11)
+    stride = 1
+    other = _fold_terms(opk, 420, 3)
+    data = [O.ct_zero() for _ in range(4)]
+    data[2] = cts[7]
+    indexes = [[0] if rng.random() < 0.8 else [rng.randrange(4)] for _ in range(len(other))]
+    indexes[5] = [3]   # slot 3: only the exp -14 literal 1 (stays the literal 1 of exp 0)
+    indexes[9] = [1]
+    v = dev_vec(pk, data)
+    v.iupdate(dev_vec(pk, other), indexes, stride, pk)
+    want = list(data)
+    O.iupdate(opk, want, other, indexes, stride)
+    assert host(pk, v) == ref(want)
+
+
 def test_chunking_cumsum_with_step(env1024):
     fx, sk, pk, coder, opk, cts = env1024
     data = cts[:24]

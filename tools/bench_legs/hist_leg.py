@@ -1,0 +1,51 @@
+"""Time the SecureBoost histogram leg of bench.py phase by phase (iupdate internals)."""
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+from fate_amd import paillier as P  # noqa: E402
+
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
+fx = json.load(open(os.path.join(ROOT, "tests", "golden", "paillier_2048.json")))
+sk, pk, coder = P.keypair_from_primes(int(fx["p"], 16), int(fx["q"], 16))
+dev = torch.device("cuda", 0)
+g = torch.Generator().manual_seed(1)
+x = (torch.randn(2 * N, generator=g) * 4).to(dev)
+gh = pk.encrypt_encoded(coder.encode_f32_vec(x), True)
+HF, NB = 4, 32
+bins = torch.randint(0, NB, (N, HF), generator=g)
+positions = bins + torch.arange(HF) * NB
+T = {}
+orig = {name: getattr(P, name) for name in ("_fold_segments", "_fold_chunks", "_fold_tree", "_add")}
+
+
+def timed(name):
+    f = orig[name]
+
+    def w(*a, **k):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        r = f(*a, **k)
+        torch.cuda.synchronize()
+        T[name] = T.get(name, 0.0) + time.perf_counter() - t0
+        return r
+    return w
+
+
+for name in orig:
+    setattr(P, name, timed(name))
+for rep in range(2):
+    T.clear()
+    hist = P.CiphertextVector.zeros(HF * NB * 2, pk._key.L2, dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    hist.iupdate(gh, positions, 2, pk)
+    torch.cuda.synchronize()
+    tot = time.perf_counter() - t0
+    print(json.dumps({"rep": rep, "total_s": round(tot, 4), "adds_per_s": round(N * HF * 2 / tot),
+                      **{k: round(v, 4) for k, v in T.items()}}), flush=True)
