@@ -619,7 +619,7 @@ __global__ __launch_bounds__(kBlock) FPHE_OCC2 void k_mul27(KeyArgs K, const u32
 // the identity of that product, so a chunk is folded as
 //   acc = t_0; acc = mont(acc, t_j) for j >= 1  (= prod t . R^-(len-1)); acc = mont(acc, R^len)
 // -- one Montgomery product per term, terms read straight from the source vector by index
-// (no gather copies).  The callers (iupdate, intervals_sum, matmul folds) group terms by
+// (element-major source, no gather copies).  The callers (iupdate, intervals_sum, matmul folds) group terms by
 // (segment, exponent) so every chunk is single-exponent; the few per-exponent partials of a
 // segment are then merged with the aligning ct-add (k_add27).  Bit-exact by the order
 // independence of the fold.
@@ -649,10 +649,19 @@ __global__ __launch_bounds__(kBlock) FPHE_OCC2 void k_fold27(KeyArgs K, const u3
   N.init(K.N2_27, g.q);
   const u32 np = K.n2_np27;
   // the 34 words of this lane's 1026-bit chunk of source element `idx` (0 past the number)
+  // Src is element-major ([element][L] words): a lane's chunk is 136 contiguous bytes, so a
+  // gathered term costs its own 512 B of lines instead of a 64-B line per 4-B word
   auto fetch = [&](int64_t idx, u32 (&W)[34]) {
-    const u32* base = Src + ((size_t)(idx >> 6) * L32 * FPHE_WAVE + (size_t)(idx & 63)) + (size_t)32 * g.q * FPHE_WAVE;
+    const uint4* b4 = reinterpret_cast<const uint4*>(Src + (size_t)idx * L32 + 32u * g.q);
 #pragma unroll
-    for (int k = 0; k < 34; ++k) W[k] = (32 * g.q + k < (int)L32) ? base[(size_t)k * FPHE_WAVE] : 0u;
+    for (int k = 0; k < 8; ++k) {
+      const uint4 v = b4[k];
+      W[4 * k] = v.x; W[4 * k + 1] = v.y; W[4 * k + 2] = v.z; W[4 * k + 3] = v.w;
+    }
+    const bool top = 32 * g.q + 32 >= (int)L32;  // the element's last lane: nothing past word L-1
+    const uint2 t = top ? make_uint2(0u, 0u) : *reinterpret_cast<const uint2*>(Src + (size_t)idx * L32 + 32u * g.q + 32u);
+    W[32] = t.x;
+    W[33] = t.y;
   };
   const u32 nwt = (u32)((nchunks + E - 1) / E);
   for (u32 wt = gw; wt < nwt; wt += nw) {
@@ -678,15 +687,26 @@ __global__ __launch_bounds__(kBlock) FPHE_OCC2 void k_fold27(KeyArgs K, const u3
       for (int k = 0; k < 34; ++k) W[k] = 0;
     }
     load_chunk(A, 2u * g.q, [&](int k) { return W[k]; });
-    if (len > 1) fetch(ord[st + 1], W);
-    // term j's words are fetched during product j-1 (software pipelined gathers)
+    // software pipeline: term j's words and sign are fetched during product j-1, and its
+    // index (ord) during product j-2, so no load latency sits in front of a product
+    u32 snext = 0;
+    if (len > 1) {
+      const int64_t i1 = ord[st + 1];
+      fetch(i1, W);
+      snext = ssign[i1];
+    }
+    int64_t inext2 = len > 2 ? ord[st + 2] : 0;
 #pragma unroll 1
     for (int j = 1; j < maxlen; ++j) {
       if (j < len) {
         load_chunk(B, 2u * g.q, [&](int k) { return W[k]; });
-        sg ^= ssign[ord[st + j]];
+        sg ^= snext;
         to_slot<TPI>(bcol, qoff, B);
-        if (j + 1 < len) fetch(ord[st + j + 1], W);
+        if (j + 1 < len) {
+          fetch(inext2, W);
+          snext = ssign[inext2];
+        }
+        inext2 = j + 2 < len ? ord[st + j + 2] : 0;
         mont_mul<TPI>(A, bcol, N, np, g.q);
       }
     }

@@ -711,6 +711,7 @@ def _flatten_positions(indexes) -> Tuple[torch.Tensor, torch.Tensor]:
 
 
 FOLD_MAX = 64  # terms per chunk of fphe_fold (kFoldMax in kernels27.h)
+FOLD_TARGET_CHUNKS = 32768
 
 
 def _run_starts(head: torch.Tensor) -> torch.Tensor:
@@ -731,12 +732,17 @@ def _fold_chunks(pk: "PK", src: CiphertextVector, ordv: torch.Tensor, keys: torc
     head = torch.ones(n, dtype=torch.bool, device=dev)
     head[1:] = keys[1:] != keys[:-1]
     gstart = _run_starts(head)
-    cstart = torch.nonzero(head | ((pos - gstart) % FOLD_MAX == 0)).squeeze(1)
+    # chunk length: 64 while that still gives every wave slot of the chip work (~32K chunks
+    # of 16-element waves), shorter on the later, smaller rounds so their sequential depth
+    # (one product per term) stays low
+    k = max(8, min(FOLD_MAX, -(-n // FOLD_TARGET_CHUNKS)))
+    cstart = torch.nonzero(head | ((pos - gstart) % k == 0)).squeeze(1)
     nch = cstart.numel()
     clen = torch.diff(cstart, append=torch.tensor([n], device=dev)).to(torch.int32)
     out = CiphertextVector.empty(nch, pk._key.L2, dev)
+    rows = src.C.permute(0, 2, 1).contiguous()  # element-major copy for the gathers
     lib = _lib.load()
-    _lib.check(lib.fphe_fold(pk._key.ctx(dev), _ptr(src.C), _ptr(src.sign), _ptr(src.exp),
+    _lib.check(lib.fphe_fold(pk._key.ctx(dev), _ptr(rows), _ptr(src.sign), _ptr(src.exp),
                              _ptr(ordv.to(torch.int64).contiguous()), _ptr(cstart.contiguous()), _ptr(clen), nch,
                              _ptr(out.C), _ptr(out.sign), _ptr(out.exp), ctypes.c_void_p(_stream(dev))), "fphe_fold")
     return out, keys[cstart]

@@ -172,7 +172,9 @@ fphe_status fphe_neg(fphe_ctx* ctx, const uint32_t* C, size_t count, uint32_t* C
  * first term.  The caller groups terms by (segment, exponent): for equal exponents the
  * reference's add is exactly this product (literal 1 is its identity), and the
  * per-exponent partials are merged with fphe_add.  ord / cstart are int64 element
- * indexes, clen int32; Co is [ceil(nchunks/64)][L2][64]. */
+ * indexes, clen int32.  Src is ELEMENT-major (uint32 [count][L2], one element's words
+ * contiguous: gathers then move whole 512-B elements); ssign / sexp flat; Co is the usual
+ * tile-major [ceil(nchunks/64)][L2][64]. */
 fphe_status fphe_fold(fphe_ctx* ctx, const uint32_t* Src, const uint8_t* ssign, const int32_t* sexp,
                       const int64_t* ord, const int64_t* cstart, const int32_t* clen, size_t nchunks,
                       uint32_t* Co, uint8_t* so, int32_t* eo, void* stream);
