@@ -147,6 +147,7 @@ def main() -> None:
     ap.add_argument("--n", type=int, default=1 << 20, help="elements per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip decrypt/add/e2e legs")
+    ap.add_argument("--no-gather", action="store_true", help="N>1: skip the ciphertext all-gather leg")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -213,6 +214,30 @@ def main() -> None:
         elapsed = float(tt.item())
     enc_kernel_ms = sum(a.elapsed_time(b) for a, b in ev_enc) / max(len(ev_enc), 1)
     value = world * N * args.steps / elapsed
+
+    # BASELINE config 5's exchange step, outside the timed region: every rank's ciphertext
+    # shard all-gathered over RCCL/xGMI (fate_amd.dist.gather_tiles), so the whole vector
+    # sits on each rank as the federation sender needs it.  Reported beside `value`.
+    gather_info = {}
+    if dist and not args.no_gather:
+        from fate_amd.dist import gather_tiles
+        barrier()
+        tg = time.perf_counter()
+        Cg, sg, eg, total = gather_tiles(ct.C, ct.sign, ct.exp, ct.count)
+        barrier()
+        gs = time.perf_counter() - tg
+        tt = torch.tensor([gs], dtype=torch.float64, device=dev)
+        tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
+        gs = float(tt.item())
+        # ciphertext bytes each rank receives (limbs + sign + exp of the other ranks' shards)
+        per_elem = ct.C.shape[1] * 4 + 1 + 4
+        recv = (total - ct.count) * per_elem
+        gather_info = {
+            "allgather": {"seconds": round(gs, 4), "elements": int(total), "bytes_per_elem": per_elem,
+                          "recv_GBps_per_rank": round(recv / gs / 1e9, 2),
+                          "encrypt_plus_allgather_per_s": round(world * N / (elapsed / args.steps + gs), 1)},
+        }
+        del Cg, sg, eg
 
     extras = {}
     if not args.no_extras:
@@ -366,6 +391,7 @@ def main() -> None:
                    "obfuscate": True, "parallelism": f"shard{world}"},
         "roofline": roofline,
     }
+    out.update(gather_info)
     out.update(extras)
     if world == 1 and not args.no_cpu_baseline:
         try:

@@ -12,7 +12,8 @@ import threading
 from typing import Optional
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libfatephe.so")
+# FPHE_LIB_PATH selects another build of the same library (A/B measurements in tools/)
+LIB_PATH = os.environ.get("FPHE_LIB_PATH") or os.path.join(_HERE, "lib", "libfatephe.so")
 
 FPHE_OK = 0
 FPHE_ERR_ARG = 1

@@ -26,6 +26,10 @@
 #include "mont_dev.h"
 #include "mont27_asm_gen.h"
 
+#ifndef FPHE_PIN_BNEXT
+#define FPHE_PIN_BNEXT 1
+#endif
+
 namespace fphe {
 namespace r27 {
 
@@ -133,6 +137,11 @@ struct Mod {
   }
 };
 
+#ifndef FPHE_FUSED
+#define FPHE_FUSED 1
+#endif
+#include "mont27_fused_gen.h"
+
 // ---- A <- A * B * R^-1 (mod N), lazy ---------------------------------------------------
 // bcol: this element's column of the wave's LDS operand tile [NL][E] (b_i at bcol[i*E]).
 // In: A limbs < 2^27 + 2^12 (almost normalised), B likewise; values < 2N (see header).
@@ -188,13 +197,30 @@ __device__ __forceinline__ void mont_mul(L27& A, const u32* bcol, const Mod<TPI>
 #pragma unroll
   for (int j = 0; j < LL; ++j) T[j] = 0;
   u32 b = bcol[0];
+  if constexpr (FPHE_FUSED && TPI > 1) {
+    // one asm block per row (mont27_fused_gen.h); the LDS read of b_{i+1} is issued before
+    // the row and waited for after it
+    const u32 mk = MASK;
+#pragma unroll 1
+    for (int i = 0; i < NL; ++i) {
+      u32 bn = bcol[(i + 1 < NL ? i + 1 : 0) * E];
+      r27f_row<TPI>(T, A, b, N, nprime, mk);
+      asm volatile("" : "+v"(bn));
+      b = bn;
+    }
+    normalize_almost<TPI>(T, A, q);
+    return;
+  }
 #pragma unroll 1
   for (int i = 0; i < NL; ++i) {
     // T += A * b_i  (LL MACs, mont27_asm_gen.h).  The memory clobbers pin the LDS read of
     // b_{i+1} between the two row blocks so its latency hides under the reduction row.
     asm volatile(R27_ASM_OPROW : R27_T_OPS(T) : R27_A_INS(A), [b] "v"(b) : "vcc", "memory");
-    const u32 bn = bcol[(i + 1 < NL ? i + 1 : 0) * E];
+    u32 bn = bcol[(i + 1 < NL ? i + 1 : 0) * E];
     red_row<TPI>(T, N, nprime, q);
+#if FPHE_PIN_BNEXT
+    asm volatile("" : "+v"(bn));
+#endif
     b = bn;
   }
   normalize_almost<TPI>(T, A, q);
@@ -224,11 +250,24 @@ __device__ __forceinline__ void sq_rows(u64 (&T)[LL], const L27& A, u32& b, cons
   const u32 b2 = b << 1;
   const u32 bf = (b << shf) & mkf;
   const u32 bl = b2 & (a < LL / 2 ? mkl0 : mkl1);
+  if constexpr (FPHE_FUSED && TPI > 1) {
+    u32 bn;
+    if constexpr (a + 1 < LL) bn = bs[(a + 1) * E];
+    else bn = bnext[0];
+    r27f_sqrow<TPI, a>(T, A, bf, b2, bl, N, nprime, MASK);
+    asm volatile("" : "+v"(bn));
+    b = bn;
+    if constexpr (a + 1 < LL) sq_rows<TPI, a + 1>(T, A, b, bs, bnext, shf, mkf, mkl0, mkl1, N, nprime, q);
+    return;
+  }
   r27_sqrow<a>(T, A, bf, b2, bl);
   u32 bn;
   if constexpr (a + 1 < LL) bn = bs[(a + 1) * E];
   else bn = bnext[0];
   red_row<TPI>(T, N, nprime, q);
+#if FPHE_PIN_BNEXT
+  asm volatile("" : "+v"(bn));  // keep the LDS wait for b_{i+1} after this row's MACs
+#endif
   b = bn;
   if constexpr (a + 1 < LL) sq_rows<TPI, a + 1>(T, A, b, bs, bnext, shf, mkf, mkl0, mkl1, N, nprime, q);
 }
