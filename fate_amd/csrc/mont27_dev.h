@@ -26,6 +26,9 @@
 #include "mont_dev.h"
 #include "mont27_asm_gen.h"
 
+#ifndef FPHE_TAB_BATCH
+#define FPHE_TAB_BATCH 1
+#endif
 #ifndef FPHE_PIN_BNEXT
 #define FPHE_PIN_BNEXT 1
 #endif
@@ -337,10 +340,18 @@ __device__ __forceinline__ void tab_load(L27& A, const Tile& t, u32 k) {
 #pragma unroll
   for (int j = 0; j < LL; j += 2) A.set2(j >> 1, t.ld((k * LL + j) * 256u), t.ld((k * LL + j + 1) * 256u));
 }
+// All LL loads are issued before the first LDS write (the scheduler otherwise pairs each
+// load with its write, and the waitcnt pass then serialises LL/2 global-memory latencies).
 template <int TPI>
 __device__ __forceinline__ void tab_to_slot(u32* bcol, u32 qoff, const Tile& t, u32 k) {
+  u32 w[LL];
 #pragma unroll
-  for (int j = 0; j < LL; ++j) bcol[qoff + j * Geo<TPI>::E] = t.ld((k * LL + j) * 256u);
+  for (int j = 0; j < LL; ++j) w[j] = t.ld((k * LL + j) * 256u);
+#if FPHE_TAB_BATCH
+  __builtin_amdgcn_sched_barrier(0);
+#endif
+#pragma unroll
+  for (int j = 0; j < LL; ++j) bcol[qoff + j * Geo<TPI>::E] = w[j];
 }
 
 // ---- exact normalisation + canonical finish -----------------------------------------------

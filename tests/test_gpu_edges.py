@@ -1,0 +1,90 @@
+"""GPU edge cases of the hot path: empty and ragged vectors (partial 64-element tiles, a
+single element, several waves), and a 2048-bit subset checked element by element against
+libgmp (oracle/gmp_ref.c, the mpz_* call sequence rug issues for paillier/src/lib.rs:94-176).
+Bit-exact on signed ciphertext integers, exponents and decoded float bits."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from fate_amd import paillier as P
+from oracle import paillier_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def load(bits):
+    with open(os.path.join(HERE, "golden", f"paillier_{bits}.json")) as f:
+        fx = json.load(f)
+    p, q = int(fx["p"], 16), int(fx["q"], 16)
+    sk, pk, coder = P.keypair_from_primes(p, q)
+    osk, opk = O.keypair_from_primes(p, q)
+    return p, q, sk, pk, coder, osk, opk
+
+
+@pytest.fixture(scope="module")
+def k1024():
+    return load(1024)
+
+
+@pytest.mark.parametrize("n", [0, 1, 63, 65, 130])
+def test_ragged_encrypt_add_mul_decrypt(k1024, n):
+    """Sizes that are not whole tiles (and the empty vector) through every element-wise op."""
+    p, q, sk, pk, coder, osk, opk = k1024
+    rng = random.Random(100 + n)
+    xs = [rng.uniform(-50, 50) for _ in range(n)]
+    ys = [rng.uniform(-1e-3, 1e-3) for _ in range(n)]  # other exponents: exercises alignment
+    ws = [rng.uniform(-2, 2) for _ in range(n)]
+    rx = [1 + rng.randrange(opk.n - 1) for _ in range(n)]
+    ry = [1 + rng.randrange(opk.n - 1) for _ in range(n)]
+    xd = torch.tensor(xs, dtype=torch.float32).cuda()
+    yd = torch.tensor(ys, dtype=torch.float32).cuda()
+    wd = torch.tensor(ws, dtype=torch.float32).cuda()
+    cx = pk.encrypt_encoded(coder.encode_f32_vec(xd), True, r=rx)
+    cy = pk.encrypt_encoded(coder.encode_f32_vec(yd), True, r=ry)
+    s = cx.add(pk, cy)
+    m = cx.mul(pk, coder.encode_f32_vec(wd))
+    dec = coder.decode_f32_vec(sk.decrypt_to_encoded(s)).cpu()
+    assert len(cx) == n and len(s) == n and len(m) == n and dec.numel() == n
+    xf = xd.cpu().tolist()
+    yf = yd.cpu().tolist()
+    wf = wd.cpu().tolist()
+    ox = [O.fp_encrypt(opk, O.encode_f32(opk.n, v), True, r) for v, r in zip(xf, rx)]
+    oy = [O.fp_encrypt(opk, O.encode_f32(opk.n, v), True, r) for v, r in zip(yf, ry)]
+    osum = [O.ct_add(opk, a, b) for a, b in zip(ox, oy)]
+    omul = [O.ct_mul(opk, a, O.encode_f32(opk.n, w)) for a, w in zip(ox, wf)]
+    assert cx.to_signed_ints(pk.ns) == ([c.c for c in ox], [c.exp for c in ox])
+    assert s.to_signed_ints(pk.ns) == ([c.c for c in osum], [c.exp for c in osum])
+    assert m.to_signed_ints(pk.ns) == ([c.c for c in omul], [c.exp for c in omul])
+    want = [float(O.decode_f32(opk.n, d.significant, d.exp)) for d in (O.fp_decrypt(osk, c) for c in osum)]
+    assert np.array(dec.tolist(), dtype=np.float32).view(np.uint32).tolist() == \
+        np.array(want, dtype=np.float32).view(np.uint32).tolist()
+
+
+def test_gmp_subset_2048():
+    """384 elements at 2048 bits (six waves of the encrypt kernel, a partial last tile)
+    against libgmp: obfuscated encrypt with injected r, nude encrypt, CRT decrypt."""
+    from oracle import gmp_ref
+    p, q, sk, pk, coder, osk, opk = load(2048)
+    gk = gmp_ref.GmpKey(p * q, p, q)
+    n = 384 - 17
+    rng = random.Random(2048)
+    xs = torch.tensor([rng.gauss(0, 4) for _ in range(n)], dtype=torch.float32)
+    pv = coder.encode_f32_vec(xs.cuda())
+    sig, exp = pv.to_ints()
+    r = [1 + rng.randrange(pk.n - 1) for _ in range(n)]
+    ct = P.PK(pk.n).encrypt_encoded(pv, True, r=r)
+    got, got_e = ct.to_signed_ints(pk.ns)
+    assert got_e == exp
+    assert got == [gk.encrypt(s, ri, True) for s, ri in zip(sig, r)]
+    nude, _ = pk.encrypt_encoded(pv, False).to_signed_ints(pk.ns)
+    assert nude == [gk.encrypt(s, None, False) for s in sig]
+    dsig, dexp = sk.decrypt_to_encoded(ct).to_ints()
+    assert dexp == exp
+    assert dsig == [gk.decrypt(c) for c in got]
+    assert dsig == [s % pk.n for s in sig]
