@@ -88,3 +88,4 @@ def test_gmp_subset_2048():
     assert dexp == exp
     assert dsig == [gk.decrypt(c) for c in got]
     assert dsig == [s % pk.n for s in sig]
+
