@@ -139,6 +139,53 @@ def cpu_baseline(p: int, q: int, seconds: float = 12.0):
     }
 
 
+def hist_packed_leg(P, pk, sk, coder, N, HF, NB, key_bits, rank, dev):
+    """SecureBoost histogram on the reference's default gh-packed path (BASELINE config 4
+    (ii); ml/ensemble/learner/decision_tree/hetero/guest.py:195-235, binary task): the guest
+    packs (g + 1, h) at precision 52 with shift_bit = compute_offset_bit(N, 2, 1), encrypts
+    one ciphertext per sample under its own key; the host folds them into HF x NB bins
+    (iupdate, all exponents 0), scans each feature (chunking_cumsum_with_step) and squeezes
+    (pack_squeeze, histogram/values/_cipher.py:141) total_pack_num = (key_bits - 2) //
+    (2 shift_bit) bins per ciphertext; the guest decrypts and unpacks
+    (_histogram_splits.py:95-104).  Checked against the float64 cumulative histogram."""
+    g0 = torch.Generator().manual_seed(4242 + rank)
+    p = torch.sigmoid(torch.randn(N, generator=g0, dtype=torch.float64))
+    y = (torch.rand(N, generator=g0, dtype=torch.float64) < 0.5).double()
+    g, h = p - y, p * (1 - p)
+    bins = torch.randint(0, NB, (N, HF), generator=g0)
+    positions = bins + torch.arange(HF) * NB
+    shift = int(math.log2(2 ** 52 * N * 2) + 1)
+    squeeze_num = (key_bits - 2) // (shift * 2)
+    vals = torch.stack([g + 1.0, h], 1).reshape(-1).to(dev)
+    t = {}
+
+    def timed(name, f):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        r = f()
+        torch.cuda.synchronize(dev)
+        t[name] = round(time.perf_counter() - t0, 4)
+        return r
+
+    pv = timed("pack_s", lambda: coder.pack_floats(vals, shift, 2, 52))
+    en = timed("encrypt_s", lambda: pk.encrypt_encoded(pv, True))
+    hist = P.CiphertextVector.zeros(HF * NB, pk._key.L2, dev)
+    timed("iupdate_s", lambda: hist.iupdate(en, positions, 1, pk))
+    timed("cumsum_s", lambda: hist.chunking_cumsum_with_step(pk, [NB] * HF, 1))
+    sq = timed("squeeze_s", lambda: hist.pack_squeeze(squeeze_num, shift * 2, pk))
+    dec = timed("decrypt_s", lambda: sk.decrypt_to_encoded(sq))
+    got = torch.tensor(coder.unpack_floats(dec, shift, 2 * squeeze_num, 52, HF * NB * 2), dtype=torch.float64)
+    want = torch.zeros(HF * NB, 2, dtype=torch.float64)
+    for f in range(HF):
+        want[:, 0].index_add_(0, positions[:, f], g + 1.0)
+        want[:, 1].index_add_(0, positions[:, f], h)
+    want = want.view(HF, NB, 2).cumsum(1).reshape(-1)
+    return {"samples": N, "features": HF, "bins": NB, "shift_bit": shift, "squeeze_num": squeeze_num,
+            "squeezed_ciphertexts": sq.count, **t,
+            "scatter_adds_per_s": round(N * HF / t["iupdate_s"], 1),
+            "allclose": bool(torch.allclose(got, want, rtol=1e-12, atol=1e-9))}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -306,6 +353,7 @@ def main() -> None:
             want[:, 1].index_add_(0, positions[:, f], xh)
         fin = torch.isfinite(want)
         hist_ok = bool(torch.allclose(hd[fin], want[fin], rtol=1e-9, atol=1e-6))
+        packed = hist_packed_leg(P, pk_kh, sk, coder, N, HF, NB, key_bits, rank, dev)
         # key-holder encryption (CRT halves): throughput, round trip, and identity with the
         # public-key path on a subset with the same injected r
         torch.cuda.synchronize(dev)
@@ -334,6 +382,7 @@ def main() -> None:
             "histogram_scatter_adds_per_s": round(N * HF * 2 / hist_s, 1),
             "histogram_config": f"{N} samples x {HF} features x {NB} bins x (g,h), iupdate fold on device",
             "histogram_allclose": hist_ok,
+            "histogram_packed": packed,
             "decrypt_per_s": round(N / (dec_ms / 1e3), 1),
             "ct_add_per_s": round(N / (add_ms / 1e3), 1),
             "e2e_host_encrypts_per_s": round(N / e2e, 1),
