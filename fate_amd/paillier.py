@@ -370,6 +370,10 @@ class CiphertextVector:
         idx = idx.to(self.device, torch.long)
         if idx.numel() == 0:
             return
+        if self.L2 != src.L2:
+            # a zeros() vector is sized before the key is known (evaluator.zeros(size, dtype),
+            # protocol/phe/paillier.py:347-349): adopt the key's limb count, exactly
+            self.C = _fit_limbs(self, src.L2).C
         srows = gather_rows(src.C, torch.arange(src.count, device=self.device)[: idx.numel()])
         self.C[idx // WAVE, :, idx % WAVE] = srows
         self.sign[idx] = src.sign[: idx.numel()]
