@@ -250,19 +250,23 @@ __device__ __forceinline__ void sq_rows(u64 (&T)[LL], const L27& A, u32& b, cons
                                         u32 shf, u32 mkf, u32 mkl0, u32 mkl1, const Mod<TPI>& N, u32 nprime,
                                         int q) {
   constexpr int E = Geo<TPI>::E;
-  const u32 b2 = b << 1;
-  const u32 bf = (b << shf) & mkf;
-  const u32 bl = b2 & (a < LL / 2 ? mkl0 : mkl1);
   if constexpr (FPHE_FUSED && TPI > 1) {
+    // fused path: the slot holds 2A (sqr), so b is already the doubled limb; shf/mkf are
+    // the bit-field offset/width that give 2b (q > s), b (q == s) or 0 (q < s) in one op
+    const u32 bf = __builtin_amdgcn_ubfe(b, shf, mkf);
+    const u32 bl = b & (a < LL / 2 ? mkl0 : mkl1);
     u32 bn;
     if constexpr (a + 1 < LL) bn = bs[(a + 1) * E];
     else bn = bnext[0];
-    r27f_sqrow<TPI, a>(T, A, bf, b2, bl, N, nprime, MASK);
+    r27f_sqrow<TPI, a>(T, A, bf, b, bl, N, nprime, MASK);
     asm volatile("" : "+v"(bn));
     b = bn;
     if constexpr (a + 1 < LL) sq_rows<TPI, a + 1>(T, A, b, bs, bnext, shf, mkf, mkl0, mkl1, N, nprime, q);
     return;
   }
+  const u32 b2 = b << 1;
+  const u32 bf = (b << shf) & mkf;
+  const u32 bl = b2 & (a < LL / 2 ? mkl0 : mkl1);
   r27_sqrow<a>(T, A, bf, b2, bl);
   u32 bn;
   if constexpr (a + 1 < LL) bn = bs[(a + 1) * E];
@@ -275,7 +279,7 @@ __device__ __forceinline__ void sq_rows(u64 (&T)[LL], const L27& A, u32& b, cons
   if constexpr (a + 1 < LL) sq_rows<TPI, a + 1>(T, A, b, bs, bnext, shf, mkf, mkl0, mkl1, N, nprime, q);
 }
 
-// bcol must hold A (to_slot) -- sqr() below does that.
+// bcol must hold A (2A on the fused path) -- sqr() below does that.
 template <int TPI>
 __device__ __forceinline__ void mont_sqr(L27& A, const u32* bcol, const Mod<TPI>& N, const u32 nprime, int q) {
   constexpr int E = Geo<TPI>::E;
@@ -285,8 +289,10 @@ __device__ __forceinline__ void mont_sqr(L27& A, const u32* bcol, const Mod<TPI>
   u32 b = bcol[0];
 #pragma unroll 1
   for (int s = 0; s < TPI; ++s) {
-    const u32 shf = q > s ? 1u : 0u;
-    const u32 mkf = q >= s ? ~0u : 0u;
+    constexpr bool kFused = FPHE_FUSED && TPI > 1;
+    // fused: bit-field (offset, width) of the doubled limb; else shift and mask of b
+    const u32 shf = kFused ? (q == s ? 1u : 0u) : (q > s ? 1u : 0u);
+    const u32 mkf = kFused ? (q > s ? 31u : (q == s ? 30u : 0u)) : (q >= s ? ~0u : 0u);
     const u32 mkl0 = q <= s ? ~0u : 0u;
     const u32 mkl1 = q < s ? ~0u : 0u;
     const u32* bs = bcol + s * LL * E;
@@ -327,7 +333,14 @@ __device__ __forceinline__ void one_to_slot(u32* bcol, u32 qoff, int q) {
 
 template <int TPI>
 __device__ __forceinline__ void sqr(L27& A, u32* bcol, u32 qoff, const Mod<TPI>& N, u32 np, int q) {
-  to_slot<TPI>(bcol, qoff, A);
+  if constexpr (FPHE_FUSED && TPI > 1) {
+    // the fused squaring rows read doubled limbs (< 2^29): 2 a_i feeds the off-diagonal
+    // MACs directly and the diagonal takes it back halved by the bit-field extract
+#pragma unroll
+    for (int j = 0; j < LL; ++j) bcol[qoff + j * Geo<TPI>::E] = A[j] << 1;
+  } else {
+    to_slot<TPI>(bcol, qoff, A);
+  }
   mont_sqr<TPI>(A, bcol, N, np, q);
 }
 
