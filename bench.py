@@ -186,6 +186,46 @@ def hist_packed_leg(P, pk, sk, coder, N, HF, NB, key_bits, rank, dev):
             "allclose": bool(torch.allclose(got, want, rtol=1e-12, atol=1e-9))}
 
 
+def hetero_lr_leg(P, pk, sk, coder, N, F, rank, dev):
+    """Hetero-LR gradient step, arbiter-centralised (BASELINE config 3;
+    ml/glm/hetero/coordinated_lr/guest.py:304-318 and host.py:242):
+      host   enc(0.25 Xw_h) under the arbiter's public key       (N obfuscated encrypts)
+      guest  enc(d) = enc(Xw_h') + (0.25 Xw - 0.5 y)              (add_plain: N ct-adds)
+      host   enc(g_h) = X_h^T enc(d)                               (rmatmul: F x N ct x pt + folds)
+      arbiter decrypts the F gradient entries.
+    Checked against the float64 computation on the same float32 inputs."""
+    g0 = torch.Generator().manual_seed(31337 + rank)
+    xw = torch.randn(N, generator=g0)
+    y = (torch.rand(N, generator=g0) < 0.5).float() * 2 - 1
+    d_plain = (0.25 * xw - 0.5 * y).to(dev)
+    xw_h = (0.25 * torch.randn(N, generator=g0)).to(dev)
+    Xh = torch.randn(N, F, generator=g0).to(dev)
+    t = {}
+
+    def timed(name, f):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        r = f()
+        torch.cuda.synchronize(dev)
+        t[name] = round(time.perf_counter() - t0, 4)
+        return r
+
+    enc_xw = timed("host_encrypt_s", lambda: pk.encrypt_encoded(coder.encode_f32_vec(xw_h), True))
+    # evaluator.add_plain (protocol/phe/paillier.py:185-191): encode + encrypt(obfuscate=False) + add
+    enc_d = timed("guest_add_plain_s",
+                  lambda: enc_xw.add(pk, pk.encrypt_encoded(coder.encode_f32_vec(d_plain), False)))
+    pt = coder.encode_f32_vec(Xh.t().contiguous().reshape(-1))
+    grad = timed("host_rmatmul_s", lambda: enc_d.rmatmul(pk, pt, [N, 1], [F, N]))
+    got = timed("arbiter_decrypt_s", lambda: coder.decode_f64_vec(sk.decrypt_to_encoded(grad))).cpu()
+    dd = (d_plain.double() + xw_h.double()).cpu()
+    want = Xh.double().cpu().t() @ dd
+    dec_d = coder.decode_f64_vec(sk.decrypt_to_encoded(enc_d)).cpu()
+    return {"samples": N, "features": F, **t,
+            "ct_x_pt_per_s": round(N * F / t["host_rmatmul_s"], 1),
+            "d_allclose": bool(torch.allclose(dec_d, dd, rtol=1e-12, atol=0)),
+            "gradient_allclose": bool(torch.allclose(got, want, rtol=1e-9, atol=1e-9))}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -354,6 +394,7 @@ def main() -> None:
         fin = torch.isfinite(want)
         hist_ok = bool(torch.allclose(hd[fin], want[fin], rtol=1e-9, atol=1e-6))
         packed = hist_packed_leg(P, pk_kh, sk, coder, N, HF, NB, key_bits, rank, dev)
+        hlr = hetero_lr_leg(P, pk, sk, coder, N, 4, rank, dev)
         # key-holder encryption (CRT halves): throughput, round trip, and identity with the
         # public-key path on a subset with the same injected r
         torch.cuda.synchronize(dev)
@@ -383,6 +424,7 @@ def main() -> None:
             "histogram_config": f"{N} samples x {HF} features x {NB} bins x (g,h), iupdate fold on device",
             "histogram_allclose": hist_ok,
             "histogram_packed": packed,
+            "hetero_lr_gradient": hlr,
             "decrypt_per_s": round(N / (dec_ms / 1e3), 1),
             "ct_add_per_s": round(N / (add_ms / 1e3), 1),
             "e2e_host_encrypts_per_s": round(N / e2e, 1),
