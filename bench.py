@@ -393,6 +393,37 @@ def main() -> None:
             want[:, 1].index_add_(0, positions[:, f], xh)
         fin = torch.isfinite(want)
         hist_ok = bool(torch.allclose(hd[fin], want[fin], rtol=1e-9, atol=1e-6))
+        hist_mgpu = None
+        if dist:
+            # config 4 across GPUs: each rank folded its own samples; the
+            # partial histograms are all-gathered over RCCL and folded again with ct-add
+            # (RCCL has no modular product; ciphertext folds are order independent)
+            try:
+                from fate_amd.dist import gather_tiles
+                barrier()
+                tg = time.perf_counter()
+                Cg, sg, eg, total = gather_tiles(hist.C, hist.sign, hist.exp, hist.count)
+                barrier()
+                t_gather = time.perf_counter() - tg
+                allp = P.CiphertextVector(Cg, sg, eg, total)
+                m = hist.count
+                tf = time.perf_counter()
+                acc = allp.slice(0, m)
+                for r in range(1, world):
+                    acc = acc.add(pk, allp.slice(r * m, m))
+                torch.cuda.synchronize(dev)
+                t_fold = time.perf_counter() - tf
+                wants = [torch.zeros_like(want) for _ in range(world)]
+                tdist.all_gather_object(wants, want)
+                want_all = sum(wants)
+                got_all = coder.decode_f64_vec(sk.decrypt_to_encoded(acc)).cpu().reshape(HF * NB, 2)
+                fin_all = torch.isfinite(want_all)
+                hist_mgpu = {"ranks": world, "gather_s": round(t_gather, 4), "fold_s": round(t_fold, 4),
+                             "allclose": bool(torch.allclose(got_all[fin_all], want_all[fin_all], rtol=1e-9,
+                                                             atol=1e-6))}
+                del Cg, sg, eg, allp, acc
+            except Exception as exc:  # report, do not take the scaling run down
+                hist_mgpu = {"error": repr(exc)[:200]}
         packed = hist_packed_leg(P, pk_kh, sk, coder, N, HF, NB, key_bits, rank, dev)
         hlr = hetero_lr_leg(P, pk, sk, coder, N, 4, rank, dev)
         # key-holder encryption (CRT halves): throughput, round trip, and identity with the
@@ -424,6 +455,7 @@ def main() -> None:
             "histogram_config": f"{N} samples x {HF} features x {NB} bins x (g,h), iupdate fold on device",
             "histogram_allclose": hist_ok,
             "histogram_packed": packed,
+            "histogram_multi_gpu": hist_mgpu,
             "hetero_lr_gradient": hlr,
             "decrypt_per_s": round(N / (dec_ms / 1e3), 1),
             "ct_add_per_s": round(N / (add_ms / 1e3), 1),
