@@ -231,7 +231,7 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--n", type=int, default=1 << 20, help="elements per GPU")
+    ap.add_argument("--n", "--elements", type=int, default=1 << 20, dest="n", help="elements per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip decrypt/add/e2e legs")
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the ciphertext all-gather leg")
@@ -243,8 +243,14 @@ def main() -> None:
     dist = world > 1
     if dist:
         import torch.distributed as tdist
+        local = local % max(1, torch.cuda.device_count())  # identity with one rank per GPU
         torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # FPHE_DIST_BACKEND=gloo: rehearse the N>1 path with several ranks on one GPU
+        backend = os.environ.get("FPHE_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            tdist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
