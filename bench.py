@@ -5,10 +5,13 @@ Workload (BASELINE.json configs[1]): 2048-bit key, float32 tensor of 2^20 elemen
 (x = randn*4, seed 20241218+rank, first 8 entries [0,-0,1e-30,-1e-30,3.4e38,-3.4e38,1,-1]),
 already resident in HBM.  One step = fixed-point encode (device) + obfuscated encryption
 (device ChaCha20 r, r^n mod n^2) of the whole batch.  N GPUs = N independent shards (weak
-scaling, one process per GPU, no collective in the timed region).  Also reported (N=1 leg
-and every rank): decrypt and ct-add throughput on the same data, the end-to-end rate with
-host->device and device->host copies, a decrypt round-trip check, the roofline of the
-dominant kernel and the CPU baseline (libgmp port of the reference call sequence).
+scaling, one process per GPU, no collective in the timed region).  Also reported (every
+rank; rank 0 prints): decrypt and ct-add throughput on the same data, the end-to-end rate
+with host->device and device->host copies, a decrypt round-trip check, key-holder (CRT)
+encryption, ct x pt, the SecureBoost histogram (unpacked and gh-packed), the Hetero-LR
+gradient step, for N>1 the ciphertext all-gather and the cross-rank histogram fold, the
+roofline of the dominant kernel and, at N=1, the CPU baseline (libgmp port of the
+reference call sequence).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--n ELEMENTS]
 """
