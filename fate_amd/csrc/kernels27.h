@@ -8,8 +8,19 @@
 #include "inv27.h"
 
 // Montgomery-engine kernels target 2 waves per SIMD (<= 256 VGPRs, no AGPR overflow): the
-// v_mad_u64_u32 stream needs two waves to issue at full rate.
+// v_mad_u64_u32 stream needs two waves to issue at full rate.  The encrypt
+// kernel runs at 3 (<= 168 VGPRs; the compiler spills ~59 dwords, touched once per general
+// row and 3 times per 38 squaring rows): +1.2-2.2% same-box; the half-size modexps of
+// decrypt and key-holder encrypt likewise (+1.5%) (profiles/r01f_ab_occ3.txt).
+#ifndef FPHE_ENC_OCC
+#define FPHE_ENC_OCC 3
+#endif
 #define FPHE_OCC2 __attribute__((amdgpu_waves_per_eu(2)))
+#define FPHE_OCC_ENC __attribute__((amdgpu_waves_per_eu(FPHE_ENC_OCC)))
+#ifndef FPHE_POW_OCC
+#define FPHE_POW_OCC 3
+#endif
+#define FPHE_OCC_POW __attribute__((amdgpu_waves_per_eu(FPHE_POW_OCC)))
 
 namespace {
 
@@ -117,7 +128,7 @@ __device__ __forceinline__ void powm27(L27& A, u32* bcol, u32 qoff, const Tile& 
 // encrypt (27-bit engine): TPI = 4 for 2048-bit keys (n^2: 152 limbs), 2 for 1024-bit.
 // ======================================================================================
 template <int L, int W>
-__global__ __launch_bounds__(kBlock) FPHE_OCC2 void k_encrypt27(KeyArgs K, const u32* __restrict__ P, u32 lp,
+__global__ __launch_bounds__(kBlock) FPHE_OCC_ENC void k_encrypt27(KeyArgs K, const u32* __restrict__ P, u32 lp,
                                                       const u8* __restrict__ neg, size_t count, int obf,
                                                       const u32* __restrict__ rin, u32* __restrict__ Cout,
                                                       u8* __restrict__ sout, u32* __restrict__ scratch, u32 ldsw) {
@@ -236,7 +247,7 @@ __device__ __forceinline__ void pow_half27(const u32* intile, u32 col, u32 inrow
 
 // In: decrypt -- ciphertexts C [T][L][64]; encrypt -- nonces r [T][L/2][64].
 template <int L, int W, bool ENC>
-__global__ __launch_bounds__(kBlock) FPHE_OCC2 void k_pow_half27(KeyArgs K, const u32* __restrict__ In, size_t count,
+__global__ __launch_bounds__(kBlock) FPHE_OCC_POW void k_pow_half27(KeyArgs K, const u32* __restrict__ In, size_t count,
                                                        u32* __restrict__ Y, u32* __restrict__ scratch, u32 ldsw) {
   constexpr int TPI = L / 64;  // p^2, q^2: 76 limbs for 2048-bit keys, 38 for 1024-bit
   using G = Geo<TPI>;
