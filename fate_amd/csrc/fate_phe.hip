@@ -1157,6 +1157,42 @@ fphe_status launch_mul27(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, con
   return hip_ok(hipGetLastError());
 }
 
+
+// ---- element permutation of tile-major vectors (gather / scatter) ---------------------
+// One thread per 32-bit word of the contiguous side, so that side is read or written fully
+// coalesced; the indexed side follows idx (stable sorts and slices keep it mostly local).
+// Indexes outside [0, nspace) are skipped; the host checks them before the call.
+template <bool SCATTER>
+__global__ __launch_bounds__(256) void k_permute(const u32* __restrict__ Cin, const u8* __restrict__ sin,
+                                                 const int32_t* __restrict__ ein, u32 L,
+                                                 const int64_t* __restrict__ idx, size_t count, size_t nspace,
+                                                 u32* __restrict__ Cout, u8* __restrict__ sout,
+                                                 int32_t* __restrict__ eout) {
+  const size_t per_tile = (size_t)L * FPHE_WAVE;
+  const size_t total = ((count + FPHE_WAVE - 1) / FPHE_WAVE) * per_tile;
+  for (size_t o = (size_t)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += (size_t)gridDim.x * blockDim.x) {
+    const size_t tile = o / per_tile, rem = o - tile * per_tile;
+    const u32 w = (u32)(rem >> 6), col = (u32)(rem & 63);
+    const size_t i = tile * FPHE_WAVE + col;  // position on the contiguous side
+    if (i >= count) continue;
+    const int64_t j = idx[i];
+    if (j < 0 || (size_t)j >= nspace) continue;
+    const size_t oj = ((size_t)j >> 6) * per_tile + (size_t)w * FPHE_WAVE + ((size_t)j & 63);
+    if (SCATTER) {
+      if (Cin) Cout[oj] = Cin[o];
+      if (w == 0) {
+        if (sin) sout[j] = sin[i];
+        if (ein) eout[j] = ein[i];
+      }
+    } else {
+      if (Cin) Cout[o] = Cin[oj];
+      if (w == 0) {
+        if (sin) sout[i] = sin[j];
+        if (ein) eout[i] = ein[j];
+      }
+    }
+  }
+}
 }  // namespace
 
 extern "C" {
@@ -1583,6 +1619,22 @@ fphe_status fphe_mul(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, const i
   if (c->L2 == 128)
     return launch_mul<128>(c, Ca, sa, ea, P, lp, pneg, pexp, p_stride, count, Co, so, eo, err, (hipStream_t)stream);
   return launch_mul<64>(c, Ca, sa, ea, P, lp, pneg, pexp, p_stride, count, Co, so, eo, err, (hipStream_t)stream);
+}
+
+fphe_status fphe_permute(const uint32_t* Cin, const uint8_t* sin, const int32_t* ein, uint32_t L,
+                         const int64_t* idx, size_t count, size_t nspace, int scatter, uint32_t* Cout,
+                         uint8_t* sout, int32_t* eout, void* stream) {
+  if (count == 0) return FPHE_OK;
+  if (!idx || L == 0 || (Cin && !Cout) || (sin && !sout) || (ein && !eout)) return FPHE_ERR_ARG;
+  const size_t words = ((count + FPHE_WAVE - 1) / FPHE_WAVE) * (size_t)L * FPHE_WAVE;
+  const unsigned grid = (unsigned)std::min<size_t>((words + 255) / 256, (size_t)1 << 20);
+  if (scatter)
+    hipLaunchKernelGGL(k_permute<true>, dim3(grid), dim3(256), 0, (hipStream_t)stream, Cin, sin, ein, L, idx, count,
+                       nspace, Cout, sout, eout);
+  else
+    hipLaunchKernelGGL(k_permute<false>, dim3(grid), dim3(256), 0, (hipStream_t)stream, Cin, sin, ein, L, idx, count,
+                       nspace, Cout, sout, eout);
+  return hipGetLastError() == hipSuccess ? FPHE_OK : FPHE_ERR_HIP;
 }
 
 }  // extern "C"

@@ -57,6 +57,36 @@ def _ptr(t: Optional[torch.Tensor]):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
+def _permute(C_in, s_in, e_in, L: int, idx: torch.Tensor, nspace: int, scatter: bool, C_out, s_out, e_out,
+             dev) -> None:
+    """fphe_permute: gather (out[i] = in[idx[i]]) or scatter (out[idx[i]] = in[i]) of
+    tile-major element vectors on the device (include/fate_phe.h)."""
+    idx = idx.to(device=dev, dtype=torch.int64).contiguous()
+    n = idx.numel()
+    if n == 0:
+        return
+    # shapes the kernel's addressing assumes (tile-major [nt, L, 64], flat sign/exp)
+    side_in, side_out = (n, nspace) if scatter else (nspace, n)
+    for t, elems in ((C_in, side_in), (C_out, side_out)):
+        if t is not None and (not t.is_contiguous() or t.dim() != 3 or t.shape[1] != L or t.shape[2] != WAVE
+                              or t.shape[0] * WAVE < elems):
+            raise ValueError(f"fphe_permute: bad tile tensor {tuple(t.shape)} for {elems} elements of {L} words")
+    for t, elems in ((s_in, side_in), (e_in, side_in), (s_out, side_out), (e_out, side_out)):
+        if t is not None and (not t.is_contiguous() or t.numel() < elems):
+            raise ValueError("fphe_permute: bad sign/exp tensor")
+    _lib.check(_lib.load().fphe_permute(_ptr(C_in), _ptr(s_in), _ptr(e_in), L, _ptr(idx), n, nspace,
+                                        1 if scatter else 0, _ptr(C_out), _ptr(s_out), _ptr(e_out),
+                                        ctypes.c_void_p(_stream(dev))), "fphe_permute")
+
+
+def _check_indexes(idx: Sequence[int], n: int) -> None:
+    """The reference indexes a Vec: an index outside [0, n) panics (slice_indexes,
+    i_shuffle: fixedpoint_paillier/src/lib.rs:457-490)."""
+    bad = [i for i in idx if not 0 <= int(i) < n]
+    if bad:
+        raise PanicException(f"index out of bounds: the len is {n} but the index is {bad[0]}")
+
+
 # --------------------------------------------------------------------------------------
 # host <-> tile-layout conversion (plumbing; not on the hot path)
 # --------------------------------------------------------------------------------------
@@ -272,9 +302,14 @@ class PlaintextVector:
         return [Plaintext(self._gather(torch.tensor([i], device=self.device))) for i in range(self.count)]
 
     def _gather(self, idx: torch.Tensor) -> "PlaintextVector":
-        idx = idx.to(self.device, torch.long)
-        return PlaintextVector(rows_to_tile_tensor(gather_rows(self.P, idx)), _pad_flat(self.neg[idx], len(idx)),
-                               _pad_flat(self.exp[idx], len(idx)), len(idx))
+        n = int(idx.numel())
+        nt = _ntiles(n)
+        dev = self.device
+        out = PlaintextVector(torch.zeros((nt, self.lp, WAVE), dtype=self.P.dtype, device=dev),
+                              torch.zeros(nt * WAVE, dtype=self.neg.dtype, device=dev),
+                              torch.zeros(nt * WAVE, dtype=self.exp.dtype, device=dev), n)
+        _permute(self.P, self.neg, self.exp, self.lp, idx, self.count, False, out.P, out.neg, out.exp, dev)
+        return out
 
     def __str__(self):
         return f"PlaintextVector(len={self.count}, lp={self.lp})"
@@ -361,9 +396,14 @@ class CiphertextVector:
 
     # ---- element plumbing (torch indexing; no arithmetic) ---------------------------
     def _gather(self, idx: torch.Tensor) -> "CiphertextVector":
-        idx = idx.to(self.device, torch.long)
-        return CiphertextVector(rows_to_tile_tensor(gather_rows(self.C, idx)), _pad_flat(self.sign[idx], len(idx)),
-                                _pad_flat(self.exp[idx], len(idx)), len(idx))
+        n = int(idx.numel())
+        nt = _ntiles(n)
+        dev = self.device
+        out = CiphertextVector(torch.zeros((nt, self.L2, WAVE), dtype=torch.int32, device=dev),
+                               torch.zeros(nt * WAVE, dtype=torch.uint8, device=dev),
+                               torch.zeros(nt * WAVE, dtype=torch.int32, device=dev), n)
+        _permute(self.C, self.sign, self.exp, self.L2, idx, self.count, False, out.C, out.sign, out.exp, dev)
+        return out
 
     def _assign(self, idx: torch.Tensor, src: "CiphertextVector") -> None:
         """self[idx[i]] = src[i] (in place; only the assigned elements move)."""
@@ -374,10 +414,7 @@ class CiphertextVector:
             # a zeros() vector is sized before the key is known (evaluator.zeros(size, dtype),
             # protocol/phe/paillier.py:347-349): adopt the key's limb count, exactly
             self.C = _fit_limbs(self, src.L2).C
-        srows = gather_rows(src.C, torch.arange(src.count, device=self.device)[: idx.numel()])
-        self.C[idx // WAVE, :, idx % WAVE] = srows
-        self.sign[idx] = src.sign[: idx.numel()]
-        self.exp[idx] = src.exp[: idx.numel()]
+        _permute(src.C, src.sign, src.exp, self.L2, idx, self.count, True, self.C, self.sign, self.exp, self.device)
 
     def slice(self, start: int, size: int) -> "CiphertextVector":
         """``CiphertextVector::slice`` (lib.rs:452-455)."""
@@ -387,7 +424,9 @@ class CiphertextVector:
 
     def slice_indexes(self, indexes: Sequence[int]) -> "CiphertextVector":
         """``CiphertextVector::slice_indexes`` (lib.rs:457-463)."""
-        return self._gather(torch.as_tensor(list(indexes), dtype=torch.long))
+        indexes = list(indexes)
+        _check_indexes(indexes, self.count)
+        return self._gather(torch.as_tensor(indexes, dtype=torch.long))
 
     def cat(self, others: Sequence["CiphertextVector"]) -> "CiphertextVector":
         """``CiphertextVector::cat`` (lib.rs:465-471)."""
@@ -403,7 +442,9 @@ class CiphertextVector:
     def i_shuffle(self, indexes: Sequence[int]) -> None:
         """``CiphertextVector::i_shuffle`` (lib.rs:473-490).  The cycle walk permutes
         data so that new[i] = old[indexes[i]] when ``indexes`` is a permutation."""
-        idx = torch.as_tensor(list(indexes), dtype=torch.long)
+        indexes = list(indexes)
+        _check_indexes(indexes, self.count)
+        idx = torch.as_tensor(indexes, dtype=torch.long)
         g = self._gather(idx)
         self.C, self.sign, self.exp = g.C, g.sign, g.exp
 

@@ -185,6 +185,16 @@ fphe_status fphe_fold(fphe_ctx* ctx, const uint32_t* Src, const uint8_t* ssign, 
 fphe_status fphe_sqmul(fphe_ctx* ctx, const uint32_t* Ca, const uint32_t* Cb, const uint8_t* sb, uint32_t nsq,
                        size_t count, uint32_t* Co, uint8_t* so, void* stream);
 
+/* Element permutation of tile-major vectors: the data movement under CiphertextVector.slice /
+ * slice_indexes / cat / i_shuffle / shuffle / iupdate and the fold plumbing (paillier.rs:
+ * 228-300; fixedpoint_paillier/src/lib.rs:452-509).  scatter = 0: out[i] = in[idx[i]];
+ * scatter = 1: out[idx[i]] = in[i]; for i < count.  C arrays are uint32 [ceil(n/64)][L][64];
+ * sign / exp flat; any of the three components may be NULL (skipped).  Indexes outside
+ * [0, nspace) are skipped.  No context: pure data movement on `stream`'s device. */
+fphe_status fphe_permute(const uint32_t* Cin, const uint8_t* sin, const int32_t* ein, uint32_t L,
+                         const int64_t* idx, size_t count, size_t nspace, int scatter, uint32_t* Cout,
+                         uint8_t* sout, int32_t* eout, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -89,3 +89,40 @@ def test_gmp_subset_2048():
     assert dsig == [gk.decrypt(c) for c in got]
     assert dsig == [s % pk.n for s in sig]
 
+
+def test_permute_gather_assign_cat():
+    """fphe_permute (gather / scatter of tile-major vectors) against torch indexing, and the
+    vector plumbing built on it: _assign, slice_indexes (with the reference's out-of-range
+    panic), cat of vectors that are not whole tiles."""
+    g = torch.Generator().manual_seed(3)
+    t = torch.randint(0, 2**31 - 1, (5, 7, 64), dtype=torch.int32, generator=g).cuda()
+    sg = torch.randint(0, 2, (320,), dtype=torch.uint8, generator=g).cuda()
+    ex = torch.randint(-20, 20, (320,), dtype=torch.int32, generator=g).cuda()
+    v = P.CiphertextVector(t.clone(), sg.clone(), ex.clone(), 317)
+    idx = torch.tensor([3, 200, 64, 0, 316, 5, 5, 130])
+    got = v._gather(idx)
+    cols = P.tiles_to_cols(t.cpu())
+    assert got.count == 8 and got.C.shape == (1, 7, 64)
+    assert torch.equal(P.tiles_to_cols(got.C.cpu())[:, :8], cols[:, idx])
+    assert torch.equal(P.tiles_to_cols(got.C.cpu())[:, 8:], torch.zeros(7, 56, dtype=torch.int32))
+    assert got.sign[:8].cpu().tolist() == sg.cpu()[idx].tolist() and got.exp[:8].cpu().tolist() == ex.cpu()[idx].tolist()
+    w = P.CiphertextVector(t.clone(), sg.clone(), ex.clone(), 317)
+    dst = torch.tensor([10, 11, 300, 12, 64, 1, 2, 3])
+    w._assign(dst, got)
+    wc = P.tiles_to_cols(w.C.cpu())
+    assert torch.equal(wc[:, dst], cols[:, idx])
+    untouched = torch.tensor([i for i in range(317) if i not in set(dst.tolist())])
+    assert torch.equal(wc[:, untouched], cols[:, untouched])
+    assert w.sign.cpu()[dst].tolist() == sg.cpu()[idx].tolist() and w.exp.cpu()[dst].tolist() == ex.cpu()[idx].tolist()
+    s2 = v.slice_indexes([316, 0, 7])
+    assert torch.equal(P.tiles_to_cols(s2.C.cpu())[:, :3], cols[:, [316, 0, 7]])
+    with pytest.raises(P.PanicException):
+        v.slice_indexes([0, 317])
+    a = P.CiphertextVector(t[:2].clone(), sg[:128].clone(), ex[:128].clone(), 100)
+    b = P.CiphertextVector(t[2:4].clone(), sg[128:256].clone(), ex[128:256].clone(), 70)
+    c = P.Evaluator.cat([a, b])
+    cc = P.tiles_to_cols(c.C.cpu())
+    assert c.count == 170
+    assert torch.equal(cc[:, :100], cols[:, :100]) and torch.equal(cc[:, 100:170], cols[:, 128:198])
+    assert c.exp[:170].cpu().tolist() == ex.cpu()[:100].tolist() + ex.cpu()[128:198].tolist()
+
