@@ -865,8 +865,9 @@ def _fold_segments(pk: "PK", src: CiphertextVector, seg: torch.Tensor, index: Op
 
 def _is_literal_one(v: CiphertextVector) -> torch.Tensor:
     """Per element: is the signed ciphertext integer exactly 1 (the reference's zero)."""
-    rows = gather_rows(v.C, torch.arange(v.count, device=v.device))
-    return (rows[:, 0] == 1) & (rows[:, 1:] == 0).all(dim=1) & (v.sign[: v.count] == 0)
+    C = v.C
+    lit = ((C[:, 0, :] == 1) & (C[:, 1:, :] == 0).all(dim=1)).reshape(-1)[: v.count]
+    return lit & (v.sign[: v.count] == 0)
 
 
 def _fold_tree(pk: "PK", src: CiphertextVector, seg: torch.Tensor) -> Tuple[CiphertextVector, torch.Tensor]:
@@ -1285,12 +1286,21 @@ class Evaluator:
         n = sum(v.count for v in vecs)
         if all(v.count % WAVE == 0 for v in vecs[:-1]):  # tile-aligned: concatenate tiles as they are
             C = torch.cat([v.C[: _ntiles(v.count)] for v in vecs], dim=0)
-        else:
-            rows = torch.cat([v.C.permute(0, 2, 1).reshape(-1, v.C.shape[1])[: v.count] for v in vecs], dim=0)
-            C = rows_to_tile_tensor(rows)
-        return CiphertextVector(C,
-                                _pad_flat(torch.cat([v.sign[: v.count] for v in vecs]), n),
-                                _pad_flat(torch.cat([v.exp[: v.count] for v in vecs]), n), n)
+            return CiphertextVector(C,
+                                    _pad_flat(torch.cat([v.sign[: v.count] for v in vecs]), n),
+                                    _pad_flat(torch.cat([v.exp[: v.count] for v in vecs]), n), n)
+        # otherwise each part is scattered to its offset (fphe_permute)
+        L2 = max(v.L2 for v in vecs)
+        dev = vecs[0].device
+        nt = _ntiles(n)
+        out = CiphertextVector(torch.zeros((nt, L2, WAVE), dtype=torch.int32, device=dev),
+                               torch.zeros(nt * WAVE, dtype=torch.uint8, device=dev),
+                               torch.zeros(nt * WAVE, dtype=torch.int32, device=dev), n)
+        off = 0
+        for v in vecs:
+            out._assign(torch.arange(off, off + v.count, device=dev), _fit_limbs(v, L2))
+            off += v.count
+        return out
 
     @staticmethod
     def slice_indexes(a: CiphertextVector, indexes: Sequence[int]) -> CiphertextVector:
