@@ -1,4 +1,7 @@
-"""Time the SecureBoost histogram leg of bench.py phase by phase (iupdate internals)."""
+"""Time the SecureBoost histogram leg of bench.py phase by phase (iupdate internals).
+With a third argument "mul", the terms are first multiplied by per-sample weights in
+[0.5, 1.5) (the weighted leg of tools/bench_legs/secureboost_full.py), which spreads their
+exponents."""
 import json
 import os
 import sys
@@ -17,11 +20,16 @@ dev = torch.device("cuda", 0)
 g = torch.Generator().manual_seed(1)
 x = (torch.randn(2 * N, generator=g) * 4).to(dev)
 gh = pk.encrypt_encoded(coder.encode_f32_vec(x), True)
-HF, NB = 4, 32
+HF = int(sys.argv[2]) if len(sys.argv) > 2 else 4
+NB = 32
+if len(sys.argv) > 3 and sys.argv[3] == "mul":
+    wts = (torch.rand(2 * N, generator=g) + 0.5).to(dev)
+    gh = gh.mul(pk, coder.encode_f32_vec(wts))
+    print(json.dumps({"distinct_exps": int(torch.unique(gh.exp[: 2 * N]).numel())}), flush=True)
 bins = torch.randint(0, NB, (N, HF), generator=g)
 positions = bins + torch.arange(HF) * NB
 T = {}
-orig = {name: getattr(P, name) for name in ("_fold_segments", "_fold_chunks", "_fold_tree", "_add")}
+orig = {name: getattr(P, name) for name in ("_fold_segments", "_fold_chunks", "_fold_tree", "_add", "_add_order")}
 
 
 def timed(name):
