@@ -34,7 +34,7 @@ EXPORTED_SYMBOLS = (
     "fphe_encode_f32", "fphe_encode_f64", "fphe_decode_f32", "fphe_decode_f64",
     "fphe_encode_i64", "fphe_decode_i64", "fphe_decode_i32", "fphe_pack_f64", "fphe_unpack_f64",
     "fphe_encrypt", "fphe_encrypt_crt", "fphe_decrypt", "fphe_add", "fphe_mul", "fphe_neg", "fphe_sqmul",
-    "fphe_fold", "fphe_permute",
+    "fphe_fold", "fphe_permute", "fphe_export_signed", "fphe_import_signed",
 )
 
 _lock = threading.Lock()
@@ -107,6 +107,9 @@ def load() -> ctypes.CDLL:
         lib.fphe_permute.argtypes = [vp, vp, vp, ctypes.c_uint32, vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int,
                                      vp, vp, vp, vp]
         lib.fphe_permute.restype = st
+        for name in ("fphe_export_signed", "fphe_import_signed"):
+            getattr(lib, name).argtypes = [vp, vp, vp, ctypes.c_size_t, vp, vp, vp]
+            getattr(lib, name).restype = st
         _lib = lib
         return lib
 

@@ -1193,6 +1193,57 @@ __global__ __launch_bounds__(256) void k_permute(const u32* __restrict__ Cin, co
     }
   }
 }
+
+// ---- (C, sign) <-> the reference's signed integers ------------------------------------
+// The reference's ciphertext is the signed rug::Integer C - sign n^2 (canonical C, SURVEY.md
+// §0 fact 1).  Export writes its magnitude as element-major LSF words and a negative flag;
+// import is the inverse.  One thread per element; the tile-major side is coalesced.
+__global__ __launch_bounds__(256) void k_export_signed(const u32* __restrict__ N2, u32 L, const u32* __restrict__ C,
+                                                       const u8* __restrict__ sign, size_t count,
+                                                       u32* __restrict__ mag, u8* __restrict__ neg) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= count) return;
+  const u32* c = C + (e >> 6) * (size_t)L * FPHE_WAVE + (e & 63);
+  u32* m = mag + e * L;
+  u32 nz = 0;
+  for (u32 w = 0; w < L; ++w) nz |= c[(size_t)w * FPHE_WAVE];
+  const bool ng = sign[e] != 0 && nz != 0;
+  u32 borrow = 0;
+  for (u32 w = 0; w < L; ++w) {
+    const u32 cw = c[(size_t)w * FPHE_WAVE];
+    if (ng) {  // n^2 - C
+      const u64 d = (u64)N2[w] - cw - borrow;
+      m[w] = (u32)d;
+      borrow = (u32)(d >> 63);
+    } else {
+      m[w] = cw;
+    }
+  }
+  neg[e] = ng ? 1 : 0;
+}
+
+__global__ __launch_bounds__(256) void k_import_signed(const u32* __restrict__ N2, u32 L, const u32* __restrict__ mag,
+                                                       const u8* __restrict__ neg, size_t count, u32* __restrict__ C,
+                                                       u8* __restrict__ sign) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= count) return;
+  u32* c = C + (e >> 6) * (size_t)L * FPHE_WAVE + (e & 63);
+  const u32* m = mag + e * L;
+  u32 nz = 0;
+  for (u32 w = 0; w < L; ++w) nz |= m[w];
+  const bool ng = neg[e] != 0 && nz != 0;
+  u32 borrow = 0;
+  for (u32 w = 0; w < L; ++w) {
+    if (ng) {  // canonical n^2 - |c|
+      const u64 d = (u64)N2[w] - m[w] - borrow;
+      c[(size_t)w * FPHE_WAVE] = (u32)d;
+      borrow = (u32)(d >> 63);
+    } else {
+      c[(size_t)w * FPHE_WAVE] = m[w];
+    }
+  }
+  sign[e] = ng ? 1 : 0;
+}
 }  // namespace
 
 extern "C" {
@@ -1635,6 +1686,28 @@ fphe_status fphe_permute(const uint32_t* Cin, const uint8_t* sin, const int32_t*
     hipLaunchKernelGGL(k_permute<false>, dim3(grid), dim3(256), 0, (hipStream_t)stream, Cin, sin, ein, L, idx, count,
                        nspace, Cout, sout, eout);
   return hipGetLastError() == hipSuccess ? FPHE_OK : FPHE_ERR_HIP;
+}
+
+fphe_status fphe_export_signed(fphe_ctx* c, const uint32_t* C, const uint8_t* sign, size_t count, uint32_t* mag,
+                               uint8_t* neg, void* stream) {
+  if (!c) return FPHE_ERR_ARG;
+  if (count == 0) return FPHE_OK;
+  if (!C || !sign || !mag || !neg) return FPHE_ERR_ARG;
+  DevGuard g(c->device);
+  hipLaunchKernelGGL(k_export_signed, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     c->K.N2, (u32)c->L2, C, sign, count, mag, neg);
+  return hip_ok(hipGetLastError());
+}
+
+fphe_status fphe_import_signed(fphe_ctx* c, const uint32_t* mag, const uint8_t* neg, size_t count, uint32_t* C,
+                               uint8_t* sign, void* stream) {
+  if (!c) return FPHE_ERR_ARG;
+  if (count == 0) return FPHE_OK;
+  if (!C || !sign || !mag || !neg) return FPHE_ERR_ARG;
+  DevGuard g(c->device);
+  hipLaunchKernelGGL(k_import_signed, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     c->K.N2, (u32)c->L2, mag, neg, count, C, sign);
+  return hip_ok(hipGetLastError());
 }
 
 }  // extern "C"

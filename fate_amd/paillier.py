@@ -386,6 +386,31 @@ class CiphertextVector:
         ex = _pad_flat(torch.tensor(list(exps), dtype=torch.int32), count).to(dev)
         return CiphertextVector(C, sign, ex, count)
 
+    def export_signed(self, pk: "PK") -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        """The reference's signed integers on the device (fphe_export_signed): magnitudes as
+        element-major LSF uint32 words [count, L2], negative flags [count], exponents."""
+        dev = self.device
+        v = _fit_limbs(self, pk._key.L2)
+        mag = torch.empty((self.count, v.L2), dtype=torch.int32, device=dev)
+        neg = torch.empty(self.count, dtype=torch.uint8, device=dev)
+        _lib.check(_lib.load().fphe_export_signed(pk._key.ctx(dev), _ptr(v.C), _ptr(v.sign), self.count, _ptr(mag),
+                                                  _ptr(neg), ctypes.c_void_p(_stream(dev))), "fphe_export_signed")
+        return mag, neg, self.exp[: self.count].clone()
+
+    @staticmethod
+    def import_signed(pk: "PK", mag: torch.Tensor, neg: torch.Tensor, exp: torch.Tensor) -> "CiphertextVector":
+        """Inverse of :meth:`export_signed` (fphe_import_signed); |value| < n^2."""
+        dev = mag.device
+        n = int(mag.shape[0])
+        if mag.dim() != 2 or mag.shape[1] != pk._key.L2 or neg.numel() != n or exp.numel() != n:
+            raise ValueError("import_signed: magnitudes [count, L2], flags and exponents [count]")
+        out = CiphertextVector.empty(n, pk._key.L2, dev)
+        _lib.check(_lib.load().fphe_import_signed(pk._key.ctx(dev), _ptr(mag.contiguous()), _ptr(neg.contiguous()), n,
+                                                  _ptr(out.C), _ptr(out.sign), ctypes.c_void_p(_stream(dev))),
+                   "fphe_import_signed")
+        out.exp[:n] = exp.to(dev, torch.int32)
+        return out
+
     # ---- pickling (wire format of this backend; see DESIGN.md) ---------------------
     def __getstate__(self):
         return {"C": self.C.cpu(), "sign": self.sign.cpu(), "exp": self.exp.cpu(), "count": self.count}

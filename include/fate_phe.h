@@ -195,6 +195,18 @@ fphe_status fphe_permute(const uint32_t* Cin, const uint8_t* sin, const int32_t*
                          const int64_t* idx, size_t count, size_t nspace, int scatter, uint32_t* Cout,
                          uint8_t* sout, int32_t* eout, void* stream);
 
+/* (7) The reference's signed ciphertext integers.  A reference Ciphertext holds the signed
+ * rug::Integer C - sign*n^2 (truncating %, fixedpoint_paillier/src/lib.rs:24-34, 301-349;
+ * paillier/src/lib.rs:35-43); this backend keeps the canonical C in [0, n^2) and the sign.
+ * export: tile-major (C, sign) -> element-major magnitude words mag[count][L2] (LSF uint32)
+ * and neg[count] (1 = negative); the wire / pickle path and parity checks use this
+ * (CiphertextVector.__getstate__, paillier.rs:219-226).  import: the inverse, for
+ * |value| < n^2 (C = n^2 - |value| for a negative value). */
+fphe_status fphe_export_signed(fphe_ctx* ctx, const uint32_t* C, const uint8_t* sign, size_t count, uint32_t* mag,
+                               uint8_t* neg, void* stream);
+fphe_status fphe_import_signed(fphe_ctx* ctx, const uint32_t* mag, const uint8_t* neg, size_t count, uint32_t* C,
+                               uint8_t* sign, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

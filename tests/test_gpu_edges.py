@@ -144,3 +144,23 @@ def test_add_gap_sorted_matches_kernel_order(k1024):
     assert s_sorted.to_signed_ints(pk.ns) == s_plain.to_signed_ints(pk.ns)
     d = coder.decode_f64_vec(sk.decrypt_to_encoded(s_sorted)).cpu()
     assert torch.allclose(d, x.double() + y.double(), rtol=1e-12, atol=0)
+
+
+@pytest.mark.parametrize("bits", [1024, 2048])
+def test_export_import_signed(bits):
+    """fphe_export_signed / fphe_import_signed against the host conversion of the fixtures'
+    signed reference integers (negative ciphertexts included)."""
+    p, q, sk, pk, coder, osk, opk = load(bits)
+    with open(os.path.join(HERE, "golden", f"paillier_{bits}.json")) as f:
+        fx = json.load(f)
+    cs = [int(c, 16) for c in fx["encrypt"]["ct"]] + [1, -1]
+    es = fx["encrypt"]["exp"] + [0, 3]
+    v = P.CiphertextVector.from_signed_ints(cs, es, pk.ns, pk._key.L2)
+    assert any(c < 0 for c in cs)
+    mag, neg, ex = v.export_signed(pk)
+    m = mag.cpu().numpy().view(np.uint32)
+    got = [(-1 if int(ng) else 1) * sum(int(w) << (32 * k) for k, w in enumerate(row))
+           for row, ng in zip(m, neg.cpu().tolist())]
+    assert got == cs and ex.cpu().tolist() == es
+    back = P.CiphertextVector.import_signed(pk, mag, neg, ex)
+    assert back.to_signed_ints(pk.ns) == (cs, es)
