@@ -817,6 +817,10 @@ struct fphe_ctx {
   KeyArgs K{};
   u32* scratch = nullptr;
   size_t scratch_bytes = 0;
+  // the stream that last used `scratch`: a call on another stream first waits for it, so
+  // two streams never share the window tables / intermediates at the same time
+  hipStream_t scratch_stream = nullptr;
+  bool scratch_used = false;
   bool r27 = true;  // reduced-radix engine (FPHE_ENGINE=32 selects the 32-bit-limb kernels)
   std::mutex mu;
 };
@@ -871,7 +875,11 @@ unsigned grid_for(const fphe_ctx* c, size_t count, int bpc) {
   return (unsigned)(g ? g : 1);
 }
 
-fphe_status ensure_scratch(fphe_ctx* c, size_t bytes) {
+fphe_status ensure_scratch(fphe_ctx* c, size_t bytes, hipStream_t s) {
+  if (c->scratch_used && c->scratch_stream != s && hipStreamSynchronize(c->scratch_stream) != hipSuccess)
+    return FPHE_ERR_HIP;
+  c->scratch_stream = s;
+  c->scratch_used = true;
   if (c->scratch_bytes >= bytes) return FPHE_OK;
   if (c->scratch) { (void)hipFree(c->scratch); c->scratch = nullptr; c->scratch_bytes = 0; }
   if (hipMalloc(&c->scratch, bytes) != hipSuccess) return FPHE_ERR_HIP;
@@ -908,7 +916,7 @@ fphe_status launch_encrypt(fphe_ctx* c, const uint32_t* P, uint32_t lp, const ui
     const size_t lds = (size_t)kWavesPerBlock * L * kHalf * 4;
     const size_t tbytes = (size_t)grid * kWavesPerBlock * (1u << kWinEnc) * LL * FPHE_WAVE * 4;
     const size_t rbytes = (size_t)ntiles_of(count) * LL * FPHE_WAVE * 4;
-    if (ensure_scratch(c, tbytes + (r ? 0 : rbytes)) != FPHE_OK) return FPHE_ERR_HIP;
+    if (ensure_scratch(c, tbytes + (r ? 0 : rbytes), s) != FPHE_OK) return FPHE_ERR_HIP;
     const u32* rbuf = r;
     if (obf && !r) {
       u32* rdev = c->scratch + tbytes / 4;
@@ -928,7 +936,7 @@ fphe_status launch_encrypt(fphe_ctx* c, const uint32_t* P, uint32_t lp, const ui
   const unsigned grid = grid_for(c, count, bpc);
   const size_t lds = (size_t)kWavesPerBlock * L * FPHE_WAVE * 4;
   const size_t sbytes = (size_t)grid * kWavesPerBlock * (1u << kWinEnc) * L * FPHE_WAVE * 4;
-  if (ensure_scratch(c, sbytes) != FPHE_OK) return FPHE_ERR_HIP;
+  if (ensure_scratch(c, sbytes, s) != FPHE_OK) return FPHE_ERR_HIP;
   ChaChaKey ck;
   for (int i = 0; i < 8; ++i) ck.k[i] = key ? key[i] : 0u;
   auto kern = k_encrypt<L, kWinEnc>;
@@ -945,7 +953,7 @@ fphe_status launch_decrypt(fphe_ctx* c, const uint32_t* C, size_t count, uint32_
   const unsigned grid = grid_for(c, count, bpc);
   const size_t lds = (size_t)kWavesPerBlock * LH * FPHE_WAVE * 4;
   const size_t sbytes = (size_t)grid * kWavesPerBlock * (1u << kWinEnc) * LH * FPHE_WAVE * 4;
-  if (ensure_scratch(c, sbytes) != FPHE_OK) return FPHE_ERR_HIP;
+  if (ensure_scratch(c, sbytes, s) != FPHE_OK) return FPHE_ERR_HIP;
   auto kern = k_decrypt<L, kWinEnc>;
   set_lds(kern, lds);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, C, ntiles_of(count), P, c->scratch);
@@ -974,7 +982,7 @@ fphe_status launch_mul(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, const
   const unsigned grid = grid_for(c, count, bpc);
   const size_t lds = (size_t)kWavesPerBlock * L * FPHE_WAVE * 4;
   const size_t sbytes = (size_t)grid * kWavesPerBlock * (1u << kWinMul) * L * FPHE_WAVE * 4;
-  if (ensure_scratch(c, sbytes) != FPHE_OK) return FPHE_ERR_HIP;
+  if (ensure_scratch(c, sbytes, s) != FPHE_OK) return FPHE_ERR_HIP;
   auto kern = k_mul<L, kWinMul>;
   set_lds(kern, lds);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, Ca, sa, ea, P, lp, pneg, pexp, pstride, count, Co,
@@ -996,7 +1004,7 @@ fphe_status launch_encrypt27(fphe_ctx* c, const uint32_t* P, uint32_t lp, const 
   const size_t tbytes = (size_t)grid * kWavesPerBlock * kTabEntries<kWinSlide> * r27::LL * FPHE_WAVE * 4;
   const size_t rbytes = (size_t)ntiles_of(count) * L1 * FPHE_WAVE * 4;
   const bool draw = obf && !r;
-  if (ensure_scratch(c, tbytes + (draw ? rbytes : 0)) != FPHE_OK) return FPHE_ERR_HIP;
+  if (ensure_scratch(c, tbytes + (draw ? rbytes : 0), s) != FPHE_OK) return FPHE_ERR_HIP;
   const u32* rbuf = r;
   if (draw) {
     u32* rdev = c->scratch + tbytes / 4;
@@ -1020,7 +1028,7 @@ fphe_status launch_decrypt27(fphe_ctx* c, const uint32_t* C, size_t count, uint3
   const unsigned grid = occ_grid(c, kern, lds, (count + E - 1) / E, "decrypt_pow27");
   const size_t tbytes = (size_t)grid * kWavesPerBlock * kTabEntries<kWinSlide> * r27::LL * FPHE_WAVE * 4;
   const size_t ybytes = (size_t)ntiles_of(count) * 2 * LH * FPHE_WAVE * 4;
-  if (ensure_scratch(c, tbytes + ybytes) != FPHE_OK) return FPHE_ERR_HIP;
+  if (ensure_scratch(c, tbytes + ybytes, s) != FPHE_OK) return FPHE_ERR_HIP;
   u32* Y = c->scratch + tbytes / 4;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, C, count, Y, c->scratch, (u32)NL);
   auto kcrt = k_decrypt_crt<L>;
@@ -1046,7 +1054,7 @@ fphe_status launch_encrypt_crt27(fphe_ctx* c, const uint32_t* P, uint32_t lp, co
   const size_t tbytes = (size_t)g1 * kWavesPerBlock * kTabEntries<kWinSlide> * r27::LL * FPHE_WAVE * 4;
   const size_t ybytes = (size_t)ntiles_of(count) * 2 * L1 * FPHE_WAVE * 4;
   const size_t rbytes = (size_t)ntiles_of(count) * L1 * FPHE_WAVE * 4;
-  if (ensure_scratch(c, tbytes + ybytes + (r ? 0 : rbytes)) != FPHE_OK) return FPHE_ERR_HIP;
+  if (ensure_scratch(c, tbytes + ybytes + (r ? 0 : rbytes), s) != FPHE_OK) return FPHE_ERR_HIP;
   u32* Y = c->scratch + tbytes / 4;
   const u32* rbuf = r;
   if (!r) {
@@ -1141,7 +1149,7 @@ fphe_status launch_mul27(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, con
   const size_t o_need = tbytes, o_eb = o_need + nt * FPHE_WAVE, o_E = o_eb + nt * FPHE_WAVE * 4;
   const size_t o_inv = o_E + nt * L1 * FPHE_WAVE * 4, o_x0 = o_inv + nt * L * FPHE_WAVE * 4;
   const size_t total = o_x0 + nt * L1 * FPHE_WAVE * 4;
-  if (ensure_scratch(c, total) != FPHE_OK) return FPHE_ERR_HIP;
+  if (ensure_scratch(c, total, s) != FPHE_OK) return FPHE_ERR_HIP;
   char* base = reinterpret_cast<char*>(c->scratch);
   u8* need = reinterpret_cast<u8*>(base + o_need);
   int32_t* eb = reinterpret_cast<int32_t*>(base + o_eb);
@@ -1635,7 +1643,7 @@ fphe_status fphe_neg(fphe_ctx* c, const uint32_t* Ca, size_t count, uint32_t* Co
   std::lock_guard<std::mutex> lk(c->mu);
   DevGuard g(c->device);
   const size_t xbytes = (size_t)ntiles_of(count) * c->L1 * FPHE_WAVE * 4;
-  if (ensure_scratch(c, xbytes) != FPHE_OK) return FPHE_ERR_HIP;
+  if (ensure_scratch(c, xbytes, (hipStream_t)stream) != FPHE_OK) return FPHE_ERR_HIP;
   if (c->L2 == 128) launch_inv27<128>(c, Ca, count, nullptr, Co, err, c->scratch, (hipStream_t)stream);
   else launch_inv27<64>(c, Ca, count, nullptr, Co, err, c->scratch, (hipStream_t)stream);
   return hip_ok(hipGetLastError());

@@ -164,3 +164,23 @@ def test_export_import_signed(bits):
     assert got == cs and ex.cpu().tolist() == es
     back = P.CiphertextVector.import_signed(pk, mag, neg, ex)
     assert back.to_signed_ints(pk.ns) == (cs, es)
+
+
+def test_two_streams_share_a_context(k1024):
+    """Encryptions issued on two HIP streams with one key context: the context's scratch
+    (window tables) is handed from one stream to the other only after the first finishes,
+    so both results decrypt exactly."""
+    p, q, sk, pk, coder, osk, opk = k1024
+    g = torch.Generator().manual_seed(17)
+    xa = (torch.randn(4096, generator=g) * 8).cuda()
+    xb = (torch.randn(6000, generator=g) * 8).cuda()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s1):
+        ca = pk.encrypt_encoded(coder.encode_f32_vec(xa), True)
+    with torch.cuda.stream(s2):
+        cb = pk.encrypt_encoded(coder.encode_f32_vec(xb), True)
+    torch.cuda.synchronize()
+    for x, c in ((xa, ca), (xb, cb)):
+        y = coder.decode_f32_vec(sk.decrypt_to_encoded(c))
+        assert torch.equal(y.cpu().view(torch.int32), x.cpu().view(torch.int32))
