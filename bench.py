@@ -436,6 +436,28 @@ def main() -> None:
                 hist_mgpu = {"error": repr(exc)[:200]}
         packed = hist_packed_leg(P, pk_kh, sk, coder, N, HF, NB, key_bits, rank, dev)
         hlr = hetero_lr_leg(P, pk, sk, coder, N, 4, rank, dev)
+        # 1024-bit keys (the reference's own tests and configs[0] use them)
+        with open(os.path.join(ROOT, "tests", "golden", "paillier_1024.json")) as f:
+            fx1 = json.load(f)
+        sk1, pk1, coder1 = P.keypair_from_primes(int(fx1["p"], 16), int(fx1["q"], 16), keyholder=False)
+        pv1 = coder1.encode_f32_vec(xd)
+        pk1.encrypt_encoded(coder1.encode_f32_vec(xd[:4096]), True)  # warm-up
+        torch.cuda.synchronize(dev)
+        e0.record(stream)
+        c1 = pk1.encrypt_encoded(pv1, True)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        enc1_ms = e0.elapsed_time(e1)
+        e0.record(stream)
+        d1 = sk1.decrypt_to_encoded(c1)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        dec1_ms = e0.elapsed_time(e1)
+        y1 = coder1.decode_f32_vec(d1)
+        k1024 = {"encrypt_per_s": round(N / (enc1_ms / 1e3), 1), "decrypt_per_s": round(N / (dec1_ms / 1e3), 1),
+                 "roundtrip_bit_exact": bool(np.array_equal(y1.cpu().numpy().view(np.uint32), xb)),
+                 "encrypt_roofline_frac": round(N * enc_mac32_per_elem(1024) / (enc1_ms / 1e3) / 1e12 / PEAK_TMAC32, 4)}
+        del c1, d1, y1, pv1
         # key-holder encryption (CRT halves): throughput, round trip, and identity with the
         # public-key path on a subset with the same injected r
         torch.cuda.synchronize(dev)
@@ -467,6 +489,7 @@ def main() -> None:
             "histogram_packed": packed,
             "histogram_multi_gpu": hist_mgpu,
             "hetero_lr_gradient": hlr,
+            "key_1024": k1024,
             "decrypt_per_s": round(N / (dec_ms / 1e3), 1),
             "ct_add_per_s": round(N / (add_ms / 1e3), 1),
             "e2e_host_encrypts_per_s": round(N / e2e, 1),
