@@ -184,3 +184,57 @@ def test_two_streams_share_a_context(k1024):
     for x, c in ((xa, ca), (xb, cb)):
         y = coder.decode_f32_vec(sk.decrypt_to_encoded(c))
         assert torch.equal(y.cpu().view(torch.int32), x.cpu().view(torch.int32))
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_random_op_chains_vs_oracle(k1024, seed):
+    """Randomised chains of the element-wise ops (add / sub / rsub / add_pt / ct x pt with
+    float, negative-float and encoded-negative-integer plaintexts / neg / i_double) over
+    vectors of random ragged length, every intermediate compared bit-exact with the oracle
+    (fixedpoint_paillier/src/lib.rs:250-349)."""
+    import random as _r
+    p, q, sk, pk, coder, osk, opk = k1024
+    rng = _r.Random(1000 + seed)
+    n = rng.randrange(1, 200)
+
+    def rand_pt():
+        k = rng.randrange(4)
+        if k == 0:
+            return O.encode_f64(opk.n, rng.uniform(-1e3, 1e3))
+        if k == 1:
+            return O.encode_f64(opk.n, rng.uniform(-1e-6, 1e-6))
+        if k == 2:
+            return O.encode_i64(opk.n, rng.randrange(-(1 << 40), 1 << 40))
+        return O.encode_f64(opk.n, float(rng.randrange(-5, 5)))
+
+    def dev_pts(pts):
+        return P.PlaintextVector.from_ints([x.significant for x in pts], [x.exp for x in pts])
+
+    oa = [O.fp_encrypt(opk, rand_pt(), True, 1 + rng.randrange(opk.n - 1)) for _ in range(n)]
+    ob = [O.fp_encrypt(opk, rand_pt(), True, 1 + rng.randrange(opk.n - 1)) for _ in range(n)]
+    da = P.CiphertextVector.from_signed_ints([c.c for c in oa], [c.exp for c in oa], pk.ns, pk._key.L2)
+    db = P.CiphertextVector.from_signed_ints([c.c for c in ob], [c.exp for c in ob], pk.ns, pk._key.L2)
+    for _ in range(6):
+        op = rng.choice(["add", "sub", "rsub", "add_pt", "mul", "neg", "double"])
+        if op == "add":
+            oa, da = [O.ct_add(opk, x, y) for x, y in zip(oa, ob)], da.add(pk, db)
+        elif op == "sub":
+            oa, da = [O.ct_sub(opk, x, y) for x, y in zip(oa, ob)], da.sub(pk, db)
+        elif op == "rsub":
+            oa, da = [O.ct_rsub(opk, x, y) for x, y in zip(oa, ob)], da.rsub(pk, db)
+        elif op == "add_pt":
+            pts = [rand_pt() for _ in range(n)]
+            enc = pk.encrypt_encoded(dev_pts(pts), False)
+            oa, da = [O.ct_add_pt(opk, x, y) for x, y in zip(oa, pts)], da.add(pk, enc)
+        elif op == "mul":
+            pts = [rand_pt() for _ in range(n)]
+            oa, da = [O.ct_mul(opk, x, y) for x, y in zip(oa, pts)], da.mul(pk, dev_pts(pts))
+        elif op == "neg":
+            oa, da = [O.ct_neg(opk, x) for x in oa], da.neg(pk)
+        else:
+            oa = [O.ct_add(opk, x, x) for x in oa]
+            da = da.add(pk, da)
+        assert da.to_signed_ints(pk.ns) == ([c.c for c in oa], [c.exp for c in oa]), op
+    got = coder.decode_f64_vec(sk.decrypt_to_encoded(da)).cpu().tolist()
+    want = [O.decode_f64(opk.n, d.significant, d.exp) for d in (O.fp_decrypt(osk, c) for c in oa)]
+    assert [float(x) for x in got] == [float(x) for x in want]
