@@ -1133,6 +1133,36 @@ void launch_inv27(fphe_ctx* c, const uint32_t* Ca, size_t count, const uint8_t* 
   hipLaunchKernelGGL(k2, dim3(g2), dim3(kBlock), lds2, s, c->K, Ca, count, need, X0, Co, (u32)NL);
 }
 
+// neg via batch inversion (kernels27.h k_binv_pre27 / k_binv_post27).  Scratch: the prefix
+// table (608 B/element at 2048 bits), the group totals, their inverses, the inverse's
+// mod-n intermediate.
+template <int L>
+fphe_status launch_neg_batch27(fphe_ctx* c, const uint32_t* Ca, size_t count, uint32_t* Co, int32_t* err,
+                               hipStream_t s) {
+  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = r27::LL * TPI, PER = FPHE_WAVE / E, KB = 4 * PER;
+  const size_t ntiles = ntiles_of(count), nwt = (ntiles + 3) / 4;
+  const size_t ntot = nwt * E;
+  const size_t tab_bytes = nwt * KB * r27::LL * FPHE_WAVE * 4;
+  const size_t tot_bytes = (size_t)ntiles_of(ntot) * L * FPHE_WAVE * 4;
+  const size_t x0_bytes = (size_t)ntiles_of(ntot) * (L / 2) * FPHE_WAVE * 4;
+  if (ensure_scratch(c, tab_bytes + 2 * tot_bytes + x0_bytes, s) != FPHE_OK) return FPHE_ERR_HIP;
+  u32* Tab = c->scratch;
+  u32* Tot = Tab + tab_bytes / 4;
+  u32* Inv = Tot + tot_bytes / 4;
+  u32* X0 = Inv + tot_bytes / 4;
+  const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
+  auto k1 = k_binv_pre27<L>;
+  set_lds(k1, lds);
+  const unsigned g1 = occ_grid(c, k1, lds, nwt, "binv_pre27");
+  hipLaunchKernelGGL(k1, dim3(g1), dim3(kBlock), lds, s, c->K, Ca, count, Tab, Tot, (u32)NL);
+  launch_inv27<L>(c, Tot, ntot, nullptr, Inv, err, X0, s);
+  auto k2 = k_binv_post27<L>;
+  set_lds(k2, lds);
+  const unsigned g2 = occ_grid(c, k2, lds, nwt, "binv_post27");
+  hipLaunchKernelGGL(k2, dim3(g2), dim3(kBlock), lds, s, c->K, Ca, count, Tab, Inv, Co, (u32)NL);
+  return hip_ok(hipGetLastError());
+}
+
 template <int L>
 fphe_status launch_mul27(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, const int32_t* ea, const uint32_t* P,
                          uint32_t lp, const uint8_t* pneg, const int32_t* pexp, int pstride, size_t count,
@@ -1642,6 +1672,12 @@ fphe_status fphe_neg(fphe_ctx* c, const uint32_t* Ca, size_t count, uint32_t* Co
   if (!Ca || !Co) return FPHE_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DevGuard g(c->device);
+  // large vectors: one inverse per group of 16 (8 at 1024 bits) elements (Montgomery's trick)
+  static const size_t kBatchMin = getenv("FPHE_NEG_BATCH_MIN") ? (size_t)atoll(getenv("FPHE_NEG_BATCH_MIN")) : 4096;
+  if (count >= kBatchMin) {
+    if (c->L2 == 128) return launch_neg_batch27<128>(c, Ca, count, Co, err, (hipStream_t)stream);
+    return launch_neg_batch27<64>(c, Ca, count, Co, err, (hipStream_t)stream);
+  }
   const size_t xbytes = (size_t)ntiles_of(count) * c->L1 * FPHE_WAVE * 4;
   if (ensure_scratch(c, xbytes, (hipStream_t)stream) != FPHE_OK) return FPHE_ERR_HIP;
   if (c->L2 == 128) launch_inv27<128>(c, Ca, count, nullptr, Co, err, c->scratch, (hipStream_t)stream);

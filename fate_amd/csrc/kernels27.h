@@ -904,4 +904,141 @@ __global__ __launch_bounds__(kBlock) FPHE_OCC2 void k_inv_lift27(KeyArgs K, cons
   }
 }
 
+
+// ======================================================================================
+// Batch inversion mod n^2 (Montgomery's trick) for neg / sub / rsub (fixedpoint_paillier/
+// src/lib.rs:259-285, invert via math/src/rug/mod.rs:30-35).  A wave owns 4 memory tiles
+// (256 elements); its element group e (TPI lanes) owns KB = 256/E of them, {tile 4w + i /
+// (64/E), column e + E (i mod 64/E)}, so every tile address stays wave-uniform.
+//   k_binv_pre27:  Pbar_i = prod_{k<=i} a_k R (Montgomery form) into the per-wave table,
+//                  and the group's total prod a_k (plain, canonical) into Tot.
+//   (the totals are inverted with k_inv_n27 + k_inv_lift27: one inverse per KB elements)
+//   k_binv_post27: walking back, a_i^-1 = I_i P_{i-1} and I_{i-1} = I_i a_i, I_i = inverse
+//                  of the prefix product.
+// 6 Montgomery products per element plus 1/KB of an inverse, against one safegcd inverse
+// and a 3-product lift per element.  Positions past `count` (and whole tiles past the
+// vector) act as 1.  A non-invertible element makes its group's total non-invertible:
+// k_inv_n27 raises FPHE_EF_NOT_INVERTIBLE (the reference panics on unwrap()).
+// ======================================================================================
+template <int TPI>
+__device__ __forceinline__ void set_one(L27& A, int q) {
+#pragma unroll
+  for (int k = 0; k < LL / 2; ++k) A.p[k] = 0;
+  if (q == 0) A.set(0, 1u);
+}
+
+template <int L>
+__global__ __launch_bounds__(kBlock) FPHE_OCC2 void k_binv_pre27(KeyArgs K, const u32* __restrict__ C, size_t count,
+                                                       u32* __restrict__ Tab, u32* __restrict__ Tot, u32 ldsw) {
+  constexpr int TPI = L / 32;
+  using G = Geo<TPI>;
+  constexpr int E = G::E, PER = FPHE_WAVE / E, KB = 4 * PER;
+  constexpr u32 L32 = L;
+  extern __shared__ __attribute__((aligned(16))) u32 lds[];
+  G g;
+  const u32 wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u32 gw = blockIdx.x * kWavesPerBlock + wib, nw = gridDim.x * kWavesPerBlock;
+  u32* bcol = lds + wib * ldsw * E + g.e;
+  const u32 qoff = lds_qoff<TPI>(g.q);
+  Mod<TPI> N;
+  N.init(K.N2_27, g.q);
+  const u32 np = K.n2_np27;
+  const u32 ntiles = (u32)((count + FPHE_WAVE - 1) / FPHE_WAVE);
+  const u32 nwt = (ntiles + 3) / 4;
+  for (u32 wt = gw; wt < nwt; wt += nw) {
+    const Tile tb = make_tile(Tab + (size_t)wt * KB * LL * FPHE_WAVE, KB * LL * 256u, g.lane);
+    L27 P;
+#pragma unroll 1
+    for (int i = 0; i < KB; ++i) {
+      const u32 tile = wt * 4 + (u32)(i / PER);
+      const u32 col = (u32)g.e + (u32)(E * (i % PER));
+      L27 A;
+      if (tile < ntiles) {  // wave-uniform
+        const ColIO Ci = colio(C + (size_t)tile * L32 * FPHE_WAVE, L32, col, 32u * g.q);
+        load_chunk(A, 2u * g.q, [&](int k) { return Ci.ld(k); });
+      }
+      const bool live = tile < ntiles && (size_t)tile * FPHE_WAVE + col < count;
+      if (!live) set_one<TPI>(A, g.q);
+      const_to_slot<TPI>(bcol, qoff, K.N2R2_27, g.q);
+      mont_mul<TPI>(A, bcol, N, np, g.q);  // a R
+      if (i == 0) {
+        P = A;
+      } else {
+        to_slot<TPI>(bcol, qoff, A);
+        mont_mul<TPI>(P, bcol, N, np, g.q);  // Pbar_i = Pbar_{i-1} a_i R / R
+      }
+      tab_store(tb, (u32)i, P);
+    }
+    one_to_slot<TPI>(bcol, qoff, g.q);
+    mont_mul<TPI>(P, bcol, N, np, g.q);  // plain prod a_k, < 2N
+    finalize<TPI>(P, N, g.q);
+    const size_t te = (size_t)wt * E + g.e;
+    const ColIO To = colio(Tot + (te >> 6) * L32 * FPHE_WAVE, L32, (u32)(te & 63), 32u * g.q);
+    store_chunk<TPI>(P, g.q, [&](int k, u32 v) { To.st(k, v); });
+  }
+}
+
+template <int L>
+__global__ __launch_bounds__(kBlock) FPHE_OCC2 void k_binv_post27(KeyArgs K, const u32* __restrict__ C, size_t count,
+                                                        const u32* __restrict__ Tab, const u32* __restrict__ Inv,
+                                                        u32* __restrict__ Co, u32 ldsw) {
+  constexpr int TPI = L / 32;
+  using G = Geo<TPI>;
+  constexpr int E = G::E, PER = FPHE_WAVE / E, KB = 4 * PER;
+  constexpr u32 L32 = L;
+  extern __shared__ __attribute__((aligned(16))) u32 lds[];
+  G g;
+  const u32 wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u32 gw = blockIdx.x * kWavesPerBlock + wib, nw = gridDim.x * kWavesPerBlock;
+  u32* bcol = lds + wib * ldsw * E + g.e;
+  const u32 qoff = lds_qoff<TPI>(g.q);
+  Mod<TPI> N;
+  N.init(K.N2_27, g.q);
+  const u32 np = K.n2_np27;
+  const u32 ntiles = (u32)((count + FPHE_WAVE - 1) / FPHE_WAVE);
+  const u32 nwt = (ntiles + 3) / 4;
+  for (u32 wt = gw; wt < nwt; wt += nw) {
+    const Tile tb = make_tile(Tab + (size_t)wt * KB * LL * FPHE_WAVE, KB * LL * 256u, g.lane);
+    L27 I;  // I_i R: Montgomery form of the inverse of a_0 ... a_i
+    {
+      const size_t te = (size_t)wt * E + g.e;
+      const ColIO Ii = colio(Inv + (te >> 6) * L32 * FPHE_WAVE, L32, (u32)(te & 63), 32u * g.q);
+      load_chunk(I, 2u * g.q, [&](int k) { return Ii.ld(k); });
+    }
+    const_to_slot<TPI>(bcol, qoff, K.N2R2_27, g.q);
+    mont_mul<TPI>(I, bcol, N, np, g.q);
+#pragma unroll 1
+    for (int i = KB - 1; i >= 0; --i) {
+      const u32 tile = wt * 4 + (u32)(i / PER);
+      const u32 col = (u32)g.e + (u32)(E * (i % PER));
+      const bool live = tile < ntiles && (size_t)tile * FPHE_WAVE + col < count;
+      // a_i^-1 = I_i P_{i-1} (I_0 for the first element)
+      L27 X = I;
+      if (i > 0) {
+        tab_to_slot<TPI>(bcol, qoff, tb, (u32)(i - 1));
+        mont_mul<TPI>(X, bcol, N, np, g.q);  // (I P) R
+      }
+      one_to_slot<TPI>(bcol, qoff, g.q);
+      mont_mul<TPI>(X, bcol, N, np, g.q);    // plain, < 2N
+      finalize<TPI>(X, N, g.q);
+      if (tile < ntiles) {  // wave-uniform; columns past count are padding of the last tile
+        const ColIO Xo = colio(Co + (size_t)tile * L32 * FPHE_WAVE, L32, col, 32u * g.q);
+        if (live) store_chunk<TPI>(X, g.q, [&](int k, u32 v) { Xo.st(k, v); });
+      }
+      if (i == 0) break;
+      // I_{i-1} = I_i a_i
+      L27 A;
+      if (tile < ntiles) {
+        const ColIO Ci = colio(C + (size_t)tile * L32 * FPHE_WAVE, L32, col, 32u * g.q);
+        load_chunk(A, 2u * g.q, [&](int k) { return Ci.ld(k); });
+      }
+      if (!live) set_one<TPI>(A, g.q);
+      const_to_slot<TPI>(bcol, qoff, K.N2R2_27, g.q);
+      mont_mul<TPI>(A, bcol, N, np, g.q);  // a_i R
+      to_slot<TPI>(bcol, qoff, A);
+      mont_mul<TPI>(I, bcol, N, np, g.q);
+    }
+  }
+}
+
 }  // namespace

@@ -59,6 +59,31 @@ def test_neg(env):
     assert host(pk, out) == ref([O.ct_neg(opk, c) for c in cts])
 
 
+@pytest.mark.parametrize("count", [4096, 8192 + 37, 3 * 4096 + 64 * 5 + 1])
+def test_neg_batch_inversion(env, count):
+    """Vectors of >= 4096 elements take the batch-inversion path (k_binv_pre27, one safegcd
+    inverse per group of 16/8 elements, k_binv_post27): ragged tails, literal 1s and
+    negative (sign 1) ciphertexts mixed in, bit-exact against the oracle's invert."""
+    fx, sk, pk, coder, opk, cts = env
+    rng = random.Random(count)
+    pool = cts + [O.ct_zero()] + [O.Ciphertext(c.c - opk.ns if c.c > 0 else c.c + opk.ns, c.exp) for c in cts[:8]]
+    want = {i: O.ct_neg(opk, c) for i, c in enumerate(pool)}
+    pick = [rng.randrange(len(pool)) for _ in range(count)]
+    out = dev_vec(pk, [pool[i] for i in pick]).neg(pk)
+    assert host(pk, out) == ref([want[i] for i in pick])
+
+
+@pytest.mark.parametrize("count", [100, 5000])
+def test_neg_not_invertible_panics(env, count):
+    """invert().unwrap() panics on a non-unit (math/src/rug/mod.rs:30-35); the batch path
+    raises it through the group total's inverse."""
+    fx, sk, pk, coder, opk, cts = env
+    bad = [cts[i % len(cts)] for i in range(count)]
+    bad[count // 3] = O.Ciphertext(int(fx["p"], 16), 0)  # shares the factor p with n^2
+    with pytest.raises(P.PanicException):
+        dev_vec(pk, bad).neg(pk)
+
+
 def test_sub_rsub(env):
     fx, sk, pk, coder, opk, cts = env
     a, b = cts[:40], cts[40:80]
@@ -295,3 +320,18 @@ def test_pack_unpack_floats(env1024):
     ct = pk.encrypt_encoded(pv, True)
     back = coder.unpack_floats(sk.decrypt_to_encoded(ct), off, pn, prec, len(vals))
     assert back == O.unpack_floats(want, off, pn, prec, len(vals))
+
+
+def test_neg_batch_inversion_full_grid(env):
+    """c * neg(c) == 1 (mod n^2) for every element of a 600k-element vector: enough wave
+    tiles that the batch-inversion kernels' grid-stride loops take several rounds (a
+    size-independent property; the element-level oracle comparison is above)."""
+    fx, sk, pk, coder, opk, cts = env
+    n = 600_000 + 17
+    g = torch.Generator().manual_seed(11)
+    x = (torch.randn(n, generator=g) * 4).cuda()
+    a = pk.encrypt_encoded(coder.encode_f32_vec(x), True)
+    prod = P._add(pk, a, P._neg(pk, a), False)
+    C = prod.C.transpose(1, 2).reshape(-1, prod.L2)[:n]  # tile-major [tiles][L2][64] -> rows
+    assert bool((C[:, 0] == 1).all()) and bool((C[:, 1:] == 0).all())
+    assert torch.equal(prod.exp[:n], a.exp[:n])
