@@ -1133,34 +1133,45 @@ void launch_inv27(fphe_ctx* c, const uint32_t* Ca, size_t count, const uint8_t* 
   hipLaunchKernelGGL(k2, dim3(g2), dim3(kBlock), lds2, s, c->K, Ca, count, need, X0, Co, (u32)NL);
 }
 
-// neg via batch inversion (kernels27.h k_binv_pre27 / k_binv_post27).  Scratch: the prefix
-// table (608 B/element at 2048 bits), the group totals, their inverses, the inverse's
-// mod-n intermediate.
+// Batch inversion mod n^2 (kernels27.h k_binv_pre27 / k_binv_post27): Co[e] = Ca[e]^-1 for
+// every element (need == nullptr) or those with need[e] != 0.  Scratch W (binv_scratch_bytes):
+// the prefix table (608 B/element at 2048 bits), the group totals, their inverses, the
+// inverse's mod-n intermediate.
 template <int L>
-fphe_status launch_neg_batch27(fphe_ctx* c, const uint32_t* Ca, size_t count, uint32_t* Co, int32_t* err,
-                               hipStream_t s) {
+size_t binv_scratch_bytes(size_t count) {
+  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, PER = FPHE_WAVE / E, KB = 4 * PER;
+  const size_t nwt = (ntiles_of(count) + 3) / 4, ntot = nwt * E;
+  return nwt * KB * r27::LL * FPHE_WAVE * 4 + 2 * (size_t)ntiles_of(ntot) * L * FPHE_WAVE * 4 +
+         (size_t)ntiles_of(ntot) * (L / 2) * FPHE_WAVE * 4;
+}
+
+// Vectors from this many elements invert by batches; shorter ones with one inverse each.
+size_t binv_min() {
+  static const size_t v = getenv("FPHE_NEG_BATCH_MIN") ? (size_t)atoll(getenv("FPHE_NEG_BATCH_MIN")) : 4096;
+  return v;
+}
+
+template <int L>
+void launch_binv27(fphe_ctx* c, const uint32_t* Ca, size_t count, const uint8_t* need, uint32_t* Co, int32_t* err,
+                   u32* W, hipStream_t s) {
   constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = r27::LL * TPI, PER = FPHE_WAVE / E, KB = 4 * PER;
-  const size_t ntiles = ntiles_of(count), nwt = (ntiles + 3) / 4;
-  const size_t ntot = nwt * E;
-  const size_t tab_bytes = nwt * KB * r27::LL * FPHE_WAVE * 4;
-  const size_t tot_bytes = (size_t)ntiles_of(ntot) * L * FPHE_WAVE * 4;
-  const size_t x0_bytes = (size_t)ntiles_of(ntot) * (L / 2) * FPHE_WAVE * 4;
-  if (ensure_scratch(c, tab_bytes + 2 * tot_bytes + x0_bytes, s) != FPHE_OK) return FPHE_ERR_HIP;
-  u32* Tab = c->scratch;
-  u32* Tot = Tab + tab_bytes / 4;
-  u32* Inv = Tot + tot_bytes / 4;
-  u32* X0 = Inv + tot_bytes / 4;
+  const size_t nwt = (ntiles_of(count) + 3) / 4, ntot = nwt * E;
+  const size_t tab_words = nwt * KB * r27::LL * FPHE_WAVE;
+  const size_t tot_words = (size_t)ntiles_of(ntot) * L * FPHE_WAVE;
+  u32* Tab = W;
+  u32* Tot = Tab + tab_words;
+  u32* Inv = Tot + tot_words;
+  u32* X0 = Inv + tot_words;
   const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
   auto k1 = k_binv_pre27<L>;
   set_lds(k1, lds);
   const unsigned g1 = occ_grid(c, k1, lds, nwt, "binv_pre27");
-  hipLaunchKernelGGL(k1, dim3(g1), dim3(kBlock), lds, s, c->K, Ca, count, Tab, Tot, (u32)NL);
+  hipLaunchKernelGGL(k1, dim3(g1), dim3(kBlock), lds, s, c->K, Ca, count, need, Tab, Tot, (u32)NL);
   launch_inv27<L>(c, Tot, ntot, nullptr, Inv, err, X0, s);
   auto k2 = k_binv_post27<L>;
   set_lds(k2, lds);
   const unsigned g2 = occ_grid(c, k2, lds, nwt, "binv_post27");
-  hipLaunchKernelGGL(k2, dim3(g2), dim3(kBlock), lds, s, c->K, Ca, count, Tab, Inv, Co, (u32)NL);
-  return hip_ok(hipGetLastError());
+  hipLaunchKernelGGL(k2, dim3(g2), dim3(kBlock), lds, s, c->K, Ca, count, need, Tab, Inv, Co, (u32)NL);
 }
 
 template <int L>
@@ -1177,8 +1188,9 @@ fphe_status launch_mul27(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, con
   const size_t nt = ntiles_of(count);
   const size_t tbytes = (size_t)grid * kWavesPerBlock * (1u << kWinMul) * r27::LL * FPHE_WAVE * 4;
   const size_t o_need = tbytes, o_eb = o_need + nt * FPHE_WAVE, o_E = o_eb + nt * FPHE_WAVE * 4;
+  const bool batch = count >= binv_min();
   const size_t o_inv = o_E + nt * L1 * FPHE_WAVE * 4, o_x0 = o_inv + nt * L * FPHE_WAVE * 4;
-  const size_t total = o_x0 + nt * L1 * FPHE_WAVE * 4;
+  const size_t total = o_x0 + (batch ? binv_scratch_bytes<L>(count) : nt * L1 * FPHE_WAVE * 4);
   if (ensure_scratch(c, total, s) != FPHE_OK) return FPHE_ERR_HIP;
   char* base = reinterpret_cast<char*>(c->scratch);
   u8* need = reinterpret_cast<u8*>(base + o_need);
@@ -1189,7 +1201,10 @@ fphe_status launch_mul27(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, con
   const unsigned pgrid = (unsigned)std::min<size_t>((count + 255) / 256, (size_t)c->cus * 8);
   hipLaunchKernelGGL(k_mul_prep<L>, dim3(pgrid), dim3(256), 0, s, c->K, P, lp, pneg, pstride, count, need, Ex, eb,
                      err);
-  launch_inv27<L>(c, Ca, count, need, Cinv, err, X0, s);
+  if (batch)
+    launch_binv27<L>(c, Ca, count, need, Cinv, err, X0, s);
+  else
+    launch_inv27<L>(c, Ca, count, need, Cinv, err, X0, s);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, Ca, Cinv, need, ea, Ex, eb, pexp, pstride, count,
                      Co, so, eo, c->scratch, (u32)NL);
   return hip_ok(hipGetLastError());
@@ -1673,10 +1688,14 @@ fphe_status fphe_neg(fphe_ctx* c, const uint32_t* Ca, size_t count, uint32_t* Co
   std::lock_guard<std::mutex> lk(c->mu);
   DevGuard g(c->device);
   // large vectors: one inverse per group of 16 (8 at 1024 bits) elements (Montgomery's trick)
-  static const size_t kBatchMin = getenv("FPHE_NEG_BATCH_MIN") ? (size_t)atoll(getenv("FPHE_NEG_BATCH_MIN")) : 4096;
-  if (count >= kBatchMin) {
-    if (c->L2 == 128) return launch_neg_batch27<128>(c, Ca, count, Co, err, (hipStream_t)stream);
-    return launch_neg_batch27<64>(c, Ca, count, Co, err, (hipStream_t)stream);
+  if (count >= binv_min()) {
+    const size_t w = c->L2 == 128 ? binv_scratch_bytes<128>(count) : binv_scratch_bytes<64>(count);
+    if (ensure_scratch(c, w, (hipStream_t)stream) != FPHE_OK) return FPHE_ERR_HIP;
+    if (c->L2 == 128)
+      launch_binv27<128>(c, Ca, count, nullptr, Co, err, c->scratch, (hipStream_t)stream);
+    else
+      launch_binv27<64>(c, Ca, count, nullptr, Co, err, c->scratch, (hipStream_t)stream);
+    return hip_ok(hipGetLastError());
   }
   const size_t xbytes = (size_t)ntiles_of(count) * c->L1 * FPHE_WAVE * 4;
   if (ensure_scratch(c, xbytes, (hipStream_t)stream) != FPHE_OK) return FPHE_ERR_HIP;

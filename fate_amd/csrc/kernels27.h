@@ -917,7 +917,8 @@ __global__ __launch_bounds__(kBlock) FPHE_OCC2 void k_inv_lift27(KeyArgs K, cons
 //                  of the prefix product.
 // 6 Montgomery products per element plus 1/KB of an inverse, against one safegcd inverse
 // and a 3-product lift per element.  Positions past `count` (and whole tiles past the
-// vector) act as 1.  A non-invertible element makes its group's total non-invertible:
+// vector), and elements with need[e] == 0 when a mask is given (the invert branches of
+// ct x pt), act as 1 and are not written.  A non-invertible element makes its group's total non-invertible:
 // k_inv_n27 raises FPHE_EF_NOT_INVERTIBLE (the reference panics on unwrap()).
 // ======================================================================================
 template <int TPI>
@@ -929,7 +930,8 @@ __device__ __forceinline__ void set_one(L27& A, int q) {
 
 template <int L>
 __global__ __launch_bounds__(kBlock) FPHE_OCC2 void k_binv_pre27(KeyArgs K, const u32* __restrict__ C, size_t count,
-                                                       u32* __restrict__ Tab, u32* __restrict__ Tot, u32 ldsw) {
+                                                       const u8* __restrict__ need, u32* __restrict__ Tab,
+                                                       u32* __restrict__ Tot, u32 ldsw) {
   constexpr int TPI = L / 32;
   using G = Geo<TPI>;
   constexpr int E = G::E, PER = FPHE_WAVE / E, KB = 4 * PER;
@@ -957,7 +959,8 @@ __global__ __launch_bounds__(kBlock) FPHE_OCC2 void k_binv_pre27(KeyArgs K, cons
         const ColIO Ci = colio(C + (size_t)tile * L32 * FPHE_WAVE, L32, col, 32u * g.q);
         load_chunk(A, 2u * g.q, [&](int k) { return Ci.ld(k); });
       }
-      const bool live = tile < ntiles && (size_t)tile * FPHE_WAVE + col < count;
+      const size_t elem = (size_t)tile * FPHE_WAVE + col;
+      const bool live = tile < ntiles && elem < count && (need == nullptr || need[elem] != 0);
       if (!live) set_one<TPI>(A, g.q);
       const_to_slot<TPI>(bcol, qoff, K.N2R2_27, g.q);
       mont_mul<TPI>(A, bcol, N, np, g.q);  // a R
@@ -980,8 +983,8 @@ __global__ __launch_bounds__(kBlock) FPHE_OCC2 void k_binv_pre27(KeyArgs K, cons
 
 template <int L>
 __global__ __launch_bounds__(kBlock) FPHE_OCC2 void k_binv_post27(KeyArgs K, const u32* __restrict__ C, size_t count,
-                                                        const u32* __restrict__ Tab, const u32* __restrict__ Inv,
-                                                        u32* __restrict__ Co, u32 ldsw) {
+                                                        const u8* __restrict__ need, const u32* __restrict__ Tab,
+                                                        const u32* __restrict__ Inv, u32* __restrict__ Co, u32 ldsw) {
   constexpr int TPI = L / 32;
   using G = Geo<TPI>;
   constexpr int E = G::E, PER = FPHE_WAVE / E, KB = 4 * PER;
@@ -1011,7 +1014,8 @@ __global__ __launch_bounds__(kBlock) FPHE_OCC2 void k_binv_post27(KeyArgs K, con
     for (int i = KB - 1; i >= 0; --i) {
       const u32 tile = wt * 4 + (u32)(i / PER);
       const u32 col = (u32)g.e + (u32)(E * (i % PER));
-      const bool live = tile < ntiles && (size_t)tile * FPHE_WAVE + col < count;
+      const size_t elem = (size_t)tile * FPHE_WAVE + col;
+      const bool live = tile < ntiles && elem < count && (need == nullptr || need[elem] != 0);
       // a_i^-1 = I_i P_{i-1} (I_0 for the first element)
       L27 X = I;
       if (i > 0) {

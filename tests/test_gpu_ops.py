@@ -129,6 +129,26 @@ def test_mul_negative_and_big_plaintexts(env):
     assert host(pk, dev_vec(pk, c).mul(pk, pv)) == ref(want)
 
 
+@pytest.mark.parametrize("count", [4096 + 3, 9000])
+def test_mul_invert_branches_batch(env, count):
+    """ct x pt over >= 4096 elements: the invert branches (negative significands, encoded
+    negative ints) take the masked batch inversion; elements that need no inverse act as 1
+    in their group.  Bit-exact against the oracle on a pool of (ct, pt) pairs."""
+    fx, sk, pk, coder, opk, cts = env
+    rng = random.Random(count)
+    pool = []
+    for i in range(64):
+        k = i % 4
+        sig = (-rng.randrange(1, 1 << 53) if k == 0 else opk.n - rng.randrange(1, 1 << 20) if k == 1
+               else rng.randrange(0, 1 << 56) if k == 2 else -1)
+        pool.append((cts[i % len(cts)], sig, rng.randrange(-20, 3)))
+    want = [O.ct_mul(opk, c, O.Plaintext(s_, e_)) for c, s_, e_ in pool]
+    pick = [rng.randrange(len(pool)) for _ in range(count)]
+    pv = P.PlaintextVector.from_ints([pool[i][1] for i in pick], [pool[i][2] for i in pick])
+    got = dev_vec(pk, [pool[i][0] for i in pick]).mul(pk, pv)
+    assert host(pk, got) == ref([want[i] for i in pick])
+
+
 def test_mul_plaintext_edges(env1024):
     """Edges of Ciphertext::mul's classification (lib.rs:334-349).  For odd n,
     max_int + 1 == n - max_int, so no significand below n is "invalid"; P > n takes the
