@@ -35,6 +35,7 @@ EXPORTED_SYMBOLS = (
     "fphe_encode_i64", "fphe_decode_i64", "fphe_decode_i32", "fphe_pack_f64", "fphe_unpack_f64",
     "fphe_encrypt", "fphe_encrypt_crt", "fphe_decrypt", "fphe_add", "fphe_mul", "fphe_neg", "fphe_sqmul",
     "fphe_fold", "fphe_permute", "fphe_export_signed", "fphe_import_signed",
+    "fphe_wire_lengths", "fphe_wire_encode", "fphe_wire_scan", "fphe_wire_decode",
 )
 
 _lock = threading.Lock()
@@ -109,6 +110,13 @@ def load() -> ctypes.CDLL:
         lib.fphe_permute.restype = st
         for name in ("fphe_export_signed", "fphe_import_signed"):
             getattr(lib, name).argtypes = [vp, vp, vp, ctypes.c_size_t, vp, vp, vp]
+            getattr(lib, name).restype = st
+        sz = ctypes.c_size_t
+        lib.fphe_wire_lengths.argtypes = [vp, vp, ctypes.c_uint32, sz, vp, vp]
+        lib.fphe_wire_encode.argtypes = [vp, vp, vp, ctypes.c_uint32, sz, vp, vp, vp, vp]
+        lib.fphe_wire_scan.argtypes = [vp, sz, sz, sz, vp, vp, vp, vp, vp, vp]
+        lib.fphe_wire_decode.argtypes = [vp, vp, vp, ctypes.c_uint32, sz, vp, vp, vp]
+        for name in ("fphe_wire_lengths", "fphe_wire_encode", "fphe_wire_scan", "fphe_wire_decode"):
             getattr(lib, name).restype = st
         _lib = lib
         return lib

@@ -1211,6 +1211,96 @@ fphe_status launch_mul27(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, con
 }
 
 
+
+// ---- wire format: bincode(serde(rug::Integer)) records (fate_utils pickles) ------------
+// A reference Ciphertext / Plaintext serializes (bincode 1.3 fixint, little endian) as
+//   i32 radix | u64 len | len ASCII chars ("-"? + digits, no leading zeros) | i32 exp
+// (BInt is a newtype over rug::Integer, math/src/rug/mod.rs:11; rug's serde writes an
+// Integer as the struct {radix, value}; pickles are bincode::serialize, paillier.rs:219-226).
+// Radix 16, lowercase.  mag is element-major LSF uint32 [count][L] (fphe_export_signed).
+__device__ __forceinline__ u32 wire_digits(const u32* __restrict__ m, u32 L) {
+  int k = (int)L - 1;
+  while (k > 0 && m[k] == 0) --k;
+  const u32 w = m[k];
+  const u32 nib = w ? (32u - (u32)__builtin_clz(w) + 3u) / 4u : 1u;
+  return (u32)k * 8u + nib;
+}
+
+__global__ __launch_bounds__(256) void k_wire_lengths(const u32* __restrict__ mag, const u8* __restrict__ neg, u32 L,
+                                                      size_t count, int64_t* __restrict__ rec_len) {
+  const size_t e = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= count) return;
+  rec_len[e] = 4 + 8 + 4 + (int64_t)(neg[e] ? 1 : 0) + (int64_t)wire_digits(mag + e * L, L);
+}
+
+// one thread per (element, 32-bit word): the word's 8 nibbles are digit positions
+// 8k .. 8k+7 from the least significant end; word 0's thread also writes the header,
+// the sign and the exponent.
+__global__ __launch_bounds__(256) void k_wire_encode(const u32* __restrict__ mag, const u8* __restrict__ neg,
+                                                     const int32_t* __restrict__ exp, u32 L, size_t count,
+                                                     const int64_t* __restrict__ rec_off,
+                                                     const int64_t* __restrict__ rec_len, u8* __restrict__ out) {
+  const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= count * L) return;
+  const size_t e = t / L;
+  const u32 k = (u32)(t % L);
+  const u32* m = mag + e * L;
+  const u32 sg = neg[e] ? 1u : 0u;
+  const u32 digits = (u32)(rec_len[e] - 16 - sg);
+  if (8u * k >= digits) return;
+  u8* r = out + rec_off[e];
+  if (k == 0) {
+    const uint64_t len = digits + sg;
+    r[0] = 16; r[1] = 0; r[2] = 0; r[3] = 0;
+    for (int b = 0; b < 8; ++b) r[4 + b] = (u8)(len >> (8 * b));
+    if (sg) r[12] = '-';
+    const u32 x = (u32)exp[e];
+    u8* ex = r + 12 + sg + digits;
+    for (int b = 0; b < 4; ++b) ex[b] = (u8)(x >> (8 * b));
+  }
+  const u32 w = m[k];
+  u8* d = r + 12 + sg;
+  for (u32 i = 0; i < 8; ++i) {
+    const u32 j = 8u * k + i;
+    if (j >= digits) break;
+    const u32 nib = (w >> (4 * i)) & 15u;
+    d[digits - 1 - j] = (u8)(nib < 10 ? '0' + nib : 'a' + nib - 10);
+  }
+}
+
+// radix-16 digit strings back to magnitude words; err bit 0: a non-hex character,
+// bit 1: more significant digits than L words hold (after leading zeros).
+__global__ __launch_bounds__(256) void k_wire_decode(const u8* __restrict__ buf, const int64_t* __restrict__ dig_off,
+                                                     const int32_t* __restrict__ dig_len, u32 L, size_t count,
+                                                     u32* __restrict__ mag, int32_t* __restrict__ err) {
+  const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= count * L) return;
+  const size_t e = t / L;
+  const u32 k = (u32)(t % L);
+  const int64_t off = dig_off[e];
+  const u32 len = (u32)dig_len[e];
+  u32 w = 0, bad = 0;
+  for (u32 i = 0; i < 8; ++i) {
+    const u32 j = 8u * k + i;
+    if (j >= len) break;
+    const u32 ch = buf[off + len - 1 - j];
+    u32 v;
+    if (ch >= '0' && ch <= '9') v = ch - '0';
+    else if (ch >= 'a' && ch <= 'f') v = ch - 'a' + 10;
+    else if (ch >= 'A' && ch <= 'F') v = ch - 'A' + 10;
+    else { v = 0; bad |= 1u; }
+    w |= v << (4 * i);
+  }
+  mag[e * L + k] = w;
+  if (k == L - 1) {  // digits past the top word must be zeros
+    for (u32 j = 8u * L; j < len; ++j) {
+      const u32 ch = buf[off + len - 1 - j];
+      if (ch != '0') { bad |= 2u; break; }
+    }
+  }
+  if (bad) atomicOr(err, (int32_t)bad);
+}
+
 // ---- element permutation of tile-major vectors (gather / scatter) ---------------------
 // One thread per 32-bit word of the contiguous side, so that side is read or written fully
 // coalesced; the indexed side follows idx (stable sorts and slices keep it mostly local).
@@ -1770,6 +1860,73 @@ fphe_status fphe_import_signed(fphe_ctx* c, const uint32_t* mag, const uint8_t* 
   DevGuard g(c->device);
   hipLaunchKernelGGL(k_import_signed, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      c->K.N2, (u32)c->L2, mag, neg, count, C, sign);
+  return hip_ok(hipGetLastError());
+}
+
+
+// ---- (8) wire format (see k_wire_encode) ----------------------------------------------
+fphe_status fphe_wire_lengths(const uint32_t* mag, const uint8_t* neg, uint32_t L, size_t count, int64_t* rec_len,
+                              void* stream) {
+  if (count == 0) return FPHE_OK;
+  if (!mag || !neg || !rec_len || L == 0) return FPHE_ERR_ARG;
+  hipLaunchKernelGGL(k_wire_lengths, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, (hipStream_t)stream, mag,
+                     neg, L, count, rec_len);
+  return hip_ok(hipGetLastError());
+}
+
+fphe_status fphe_wire_encode(const uint32_t* mag, const uint8_t* neg, const int32_t* exp, uint32_t L, size_t count,
+                             const int64_t* rec_off, const int64_t* rec_len, uint8_t* out, void* stream) {
+  if (count == 0) return FPHE_OK;
+  if (!mag || !neg || !exp || !rec_off || !rec_len || !out || L == 0) return FPHE_ERR_ARG;
+  const size_t threads = count * L;
+  hipLaunchKernelGGL(k_wire_encode, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, (hipStream_t)stream, mag,
+                     neg, exp, L, count, rec_off, rec_len, out);
+  return hip_ok(hipGetLastError());
+}
+
+fphe_status fphe_wire_scan(const uint8_t* buf, size_t nbytes, size_t pos, size_t count, int64_t* dig_off,
+                           int32_t* dig_len, uint8_t* neg, int32_t* exp, int32_t* radix, size_t* end) {
+  if (!buf && nbytes) return FPHE_ERR_ARG;
+  if (count && (!dig_off || !dig_len || !neg || !exp || !radix)) return FPHE_ERR_ARG;
+  auto rd = [&](size_t at, int nb) {
+    uint64_t v = 0;
+    for (int b = 0; b < nb; ++b) v |= (uint64_t)buf[at + b] << (8 * b);
+    return v;
+  };
+  for (size_t e = 0; e < count; ++e) {
+    if (pos + 12 > nbytes) return FPHE_ERR_ARG;
+    const int32_t rdx = (int32_t)(uint32_t)rd(pos, 4);
+    const uint64_t len = rd(pos + 4, 8);
+    pos += 12;
+    if (rdx < 2 || rdx > 36 || len == 0 || len > nbytes - pos || nbytes - pos - len < 4) return FPHE_ERR_ARG;
+    size_t d = pos, n = (size_t)len;
+    uint8_t sg = 0;
+    if (buf[d] == '-' || buf[d] == '+') {
+      sg = buf[d] == '-';
+      ++d;
+      --n;
+      if (n == 0) return FPHE_ERR_ARG;
+    }
+    if (n > INT32_MAX) return FPHE_ERR_ARG;
+    dig_off[e] = (int64_t)d;
+    dig_len[e] = (int32_t)n;
+    neg[e] = sg;
+    radix[e] = rdx;
+    pos += (size_t)len;
+    exp[e] = (int32_t)(uint32_t)rd(pos, 4);
+    pos += 4;
+  }
+  if (end) *end = pos;
+  return FPHE_OK;
+}
+
+fphe_status fphe_wire_decode(const uint8_t* buf, const int64_t* dig_off, const int32_t* dig_len, uint32_t L,
+                             size_t count, uint32_t* mag, int32_t* err, void* stream) {
+  if (count == 0) return FPHE_OK;
+  if (!buf || !dig_off || !dig_len || !mag || !err || L == 0) return FPHE_ERR_ARG;
+  const size_t threads = count * L;
+  hipLaunchKernelGGL(k_wire_decode, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, (hipStream_t)stream, buf,
+                     dig_off, dig_len, L, count, mag, err);
   return hip_ok(hipGetLastError());
 }
 

@@ -405,7 +405,8 @@ class CiphertextVector:
         if mag.dim() != 2 or mag.shape[1] != pk._key.L2 or neg.numel() != n or exp.numel() != n:
             raise ValueError("import_signed: magnitudes [count, L2], flags and exponents [count]")
         out = CiphertextVector.empty(n, pk._key.L2, dev)
-        _lib.check(_lib.load().fphe_import_signed(pk._key.ctx(dev), _ptr(mag.contiguous()), _ptr(neg.contiguous()), n,
+        mag, neg = mag.contiguous(), neg.contiguous()  # held across the launch
+        _lib.check(_lib.load().fphe_import_signed(pk._key.ctx(dev), _ptr(mag), _ptr(neg), n,
                                                   _ptr(out.C), _ptr(out.sign), ctypes.c_void_p(_stream(dev))),
                    "fphe_import_signed")
         out.exp[:n] = exp.to(dev, torch.int32)
@@ -848,8 +849,11 @@ def _fold_chunks(pk: "PK", src: CiphertextVector, ordv: torch.Tensor, keys: torc
     out = CiphertextVector.empty(nch, pk._key.L2, dev)
     rows = src.C.permute(0, 2, 1).contiguous()  # element-major copy for the gathers
     lib = _lib.load()
+    # operands bound to names: a temporary passed as _ptr(t.to(...)) would go back to the
+    # caching allocator before the launch and could share its block with the next one
+    ord64, cst = ordv.to(torch.int64).contiguous(), cstart.contiguous()
     _lib.check(lib.fphe_fold(pk._key.ctx(dev), _ptr(rows), _ptr(src.sign), _ptr(src.exp),
-                             _ptr(ordv.to(torch.int64).contiguous()), _ptr(cstart.contiguous()), _ptr(clen), nch,
+                             _ptr(ord64), _ptr(cst), _ptr(clen), nch,
                              _ptr(out.C), _ptr(out.sign), _ptr(out.exp), ctypes.c_void_p(_stream(dev))), "fphe_fold")
     return out, keys[cstart]
 

@@ -207,6 +207,30 @@ fphe_status fphe_export_signed(fphe_ctx* ctx, const uint32_t* C, const uint8_t* 
 fphe_status fphe_import_signed(fphe_ctx* ctx, const uint32_t* mag, const uint8_t* neg, size_t count, uint32_t* C,
                                uint8_t* sign, void* stream);
 
+/* (8) Wire format of the reference's pickles: bincode 1.3 (fixint, little endian) of serde
+ * structs whose big integers are rug::Integer, which rug's serde writes as {radix: i32,
+ * value: String}.  Per element (fixedpoint_paillier Ciphertext / Plaintext, lib.rs:237-241,
+ * 358-362): i32 radix | u64 len | "-"? digits | i32 exp; a vector is u64 count + elements
+ * (CiphertextVector.__getstate__ / __setstate__, paillier.rs:219-226).  Radix 16 lowercase
+ * is written.  The byte layout follows rug 1.20's published serde code and is not pinned
+ * against a real rug build (none in this image).  No context: pure data formatting.
+ *   fphe_wire_lengths: rec_len[e] = bytes of element e's record (device).
+ *   fphe_wire_encode:  records at out + rec_off[e] (device; rec_off = exclusive scan of
+ *                      the rec_len that fphe_wire_lengths wrote for the same mag / neg).
+ *   fphe_wire_scan:    HOST walk of `count` records from buf + pos: digit offsets/lengths,
+ *                      sign, exp, radix per element; *end = offset after the last record.
+ *                      FPHE_ERR_ARG on a truncated record or a radix outside 2..36.
+ *   fphe_wire_decode:  radix-16 digit strings -> mag[count][L] (device); err |= 1 for a
+ *                      non-hex digit, 2 for a value wider than L words. */
+fphe_status fphe_wire_lengths(const uint32_t* mag, const uint8_t* neg, uint32_t L, size_t count, int64_t* rec_len,
+                              void* stream);
+fphe_status fphe_wire_encode(const uint32_t* mag, const uint8_t* neg, const int32_t* exp, uint32_t L, size_t count,
+                             const int64_t* rec_off, const int64_t* rec_len, uint8_t* out, void* stream);
+fphe_status fphe_wire_scan(const uint8_t* buf, size_t nbytes, size_t pos, size_t count, int64_t* dig_off,
+                           int32_t* dig_len, uint8_t* neg, int32_t* exp, int32_t* radix, size_t* end);
+fphe_status fphe_wire_decode(const uint8_t* buf, const int64_t* dig_off, const int32_t* dig_len, uint32_t L,
+                             size_t count, uint32_t* mag, int32_t* err, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,152 @@
+"""Wire format of the reference's pickles (fate_amd/wire.py; bincode(serde) of
+fate_utils.paillier objects, paillier.rs:67-74,91-98,128-135,219-226,395-402).  The rug
+Integer record layout is unpinned (no rug / bincode in this image): these tests pin the
+layout as documented in include/fate_phe.h (8) and check device encode/decode against a
+record-by-record construction written here from the spec, plus round trips."""
+import json
+import os
+import struct
+
+import numpy as np
+import pytest
+import torch
+
+from fate_amd import _lib, wire
+from fate_amd import paillier as P
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def fixture(bits):
+    with open(os.path.join(HERE, "golden", f"paillier_{bits}.json")) as f:
+        return json.load(f)
+
+
+def rec(v, radix=16):
+    """One rug Integer record built from the spec: i32 radix, u64 len, sign + digits."""
+    digs = "0123456789abcdefghijklmnopqrstuvwxyz"
+    m, out = abs(v), ""
+    while True:
+        m, d = divmod(m, radix)
+        out = digs[d] + out
+        if m == 0:
+            break
+    s = ("-" if v < 0 else "") + out
+    return struct.pack("<i", radix) + struct.pack("<Q", len(s)) + s.encode()
+
+
+def ct_vec_bytes(cs, es, radix=16):
+    return struct.pack("<Q", len(cs)) + b"".join(rec(c, radix) + struct.pack("<i", e) for c, e in zip(cs, es))
+
+
+def test_bint_records():
+    assert wire.bint(0) == struct.pack("<iQ", 16, 1) + b"0"
+    assert wire.bint(-255) == struct.pack("<iQ", 16, 3) + b"-ff"
+    for v in (1, -1, 2**64, -(2**4095 + 12345), 0xDEADBEEF):
+        assert wire.bint(v) == rec(v)
+        assert wire.Reader(rec(v)).bint() == v
+        assert wire.Reader(rec(v, 10)).bint() == v  # any radix reads back
+    with pytest.raises(ValueError):
+        wire.Reader(rec(5)[:-1]).bint()
+    with pytest.raises(ValueError):
+        wire.Reader(struct.pack("<iQ", 40, 1) + b"1").bint()
+
+
+def test_key_and_coder_records():
+    fx = fixture(1024)
+    p, q = int(fx["p"], 16), int(fx["q"], 16)
+    n = p * q
+    sk, pk, coder = P.keypair_from_primes(p, q)
+    b = wire.pk_to_bincode(pk)
+    assert b == rec(n) + rec(n * n) + rec(n // 2)
+    assert wire.pk_from_bincode(b).n == n
+    lo, hi = min(p, q), max(p, q)
+    g = n + 1
+    hp = pow((pow(g, lo - 1, lo * lo) - 1) // lo, -1, lo)
+    hq = pow((pow(g, hi - 1, hi * hi) - 1) // hi, -1, hi)
+    want = [lo, hi, n, lo - 1, hi - 1, lo * lo, hi * hi, pow(lo, -1, hi), hp, hq]
+    b = wire.sk_to_bincode(sk)
+    assert b == b"".join(rec(v) for v in want)
+    back = wire.sk_from_bincode(b)
+    assert (back.p, back.q) == (lo, hi)
+    assert wire.coder_to_bincode(n) == rec(n) + rec(n // 2)
+    assert wire.coder_from_bincode(wire.coder_to_bincode(n)) == n
+    with pytest.raises(ValueError):
+        wire.pk_from_bincode(rec(n) + rec(n * n + 1) + rec(n // 2))
+
+
+def test_scan_walks_records():
+    """fphe_wire_scan (host code in the C ABI library): offsets, signs, exps, radixes."""
+    lib = _lib.load()
+    cs, es = [0, -5, 2**100 + 7, 255], [-14, 3, 0, -2**31]
+    buf = ct_vec_bytes(cs[:2], es[:2]) + ct_vec_bytes(cs[2:], es[2:], radix=10)[8:]
+    raw = np.frombuffer(buf, dtype=np.uint8)
+    n = len(cs)
+    off, ln = np.empty(n, np.int64), np.empty(n, np.int32)
+    neg, ex, rdx = np.empty(n, np.uint8), np.empty(n, np.int32), np.empty(n, np.int32)
+    import ctypes
+    end = ctypes.c_size_t(0)
+    st = lib.fphe_wire_scan(raw.ctypes.data, raw.size, 8, n, off.ctypes.data, ln.ctypes.data, neg.ctypes.data,
+                            ex.ctypes.data, rdx.ctypes.data, ctypes.byref(end))
+    assert st == 0 and end.value == len(buf)
+    assert ex.tolist() == es and neg.tolist() == [0, 1, 0, 0] and rdx.tolist() == [16, 16, 10, 10]
+    for i, c in enumerate(cs):
+        txt = buf[off[i]: off[i] + ln[i]].decode()
+        assert int(txt, int(rdx[i])) == abs(c)
+    st = lib.fphe_wire_scan(raw.ctypes.data, raw.size - 1, 8, n, off.ctypes.data, ln.ctypes.data, neg.ctypes.data,
+                            ex.ctypes.data, rdx.ctypes.data, ctypes.byref(end))
+    assert st != 0  # truncated
+
+
+def _dev_cts(bits, count, seed):
+    fx = fixture(bits)
+    p, q = int(fx["p"], 16), int(fx["q"], 16)
+    sk, pk, coder = P.keypair_from_primes(p, q)
+    cs0 = [int(c, 16) for c in fx["encrypt"]["ct"]]
+    es0 = list(fx["encrypt"]["exp"])
+    rng = np.random.default_rng(seed)
+    pick = rng.integers(0, len(cs0), count).tolist()
+    cs, es = [cs0[i] for i in pick], [es0[i] for i in pick]
+    cs[:3] = [1, 0, -(p * q) ** 2 + 1][:min(3, count)]  # literal 1, zero, most negative
+    es[:3] = [0, -14, 5][:min(3, count)]
+    cv = P.CiphertextVector.from_signed_ints(cs, es, pk.ns, pk._key.L2)
+    return pk, cv, cs, es
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits,count", [(1024, 1), (1024, 300), (2048, 4097)])
+def test_ciphertext_vector_device_codec(bits, count):
+    pk, cv, cs, es = _dev_cts(bits, count, count)
+    b = wire.ciphertext_vector_to_bincode(cv, pk)
+    assert b == ct_vec_bytes(cs, es)
+    back, used = wire.ciphertext_vector_from_bincode(b + b"tail", pk)
+    assert used == len(b)
+    assert back.to_signed_ints(pk.ns) == (cs, es)
+
+
+@pytest.mark.gpu
+def test_ciphertext_vector_decode_other_radix_and_errors():
+    pk, cv, cs, es = _dev_cts(1024, 40, 1)
+    back, _ = wire.ciphertext_vector_from_bincode(ct_vec_bytes(cs, es, radix=10), pk)
+    assert back.to_signed_ints(pk.ns) == (cs, es)
+    up = ct_vec_bytes(cs, es).replace(b"a", b"A")  # uppercase hex digits are accepted
+    assert wire.ciphertext_vector_from_bincode(up, pk)[0].to_signed_ints(pk.ns) == (cs, es)
+    with pytest.raises(ValueError):  # |c| >= n^2
+        wire.ciphertext_vector_from_bincode(ct_vec_bytes([pk.ns], [0]), pk)
+    with pytest.raises(ValueError):  # non-digit
+        wire.ciphertext_vector_from_bincode(struct.pack("<QiQ", 1, 16, 3) + b"1g2" + struct.pack("<i", 0), pk)
+    with pytest.raises(ValueError):  # truncated
+        wire.ciphertext_vector_from_bincode(ct_vec_bytes(cs, es)[:-2], pk)
+    empty, used = wire.ciphertext_vector_from_bincode(struct.pack("<Q", 0), pk)
+    assert empty.count == 0 and used == 8
+
+
+@pytest.mark.gpu
+def test_plaintext_vector_codec():
+    fx = fixture(1024)
+    sk, pk, coder = P.keypair_from_primes(int(fx["p"], 16), int(fx["q"], 16))
+    sigs, exps = [0, -3, 2**60 + 1, pk.n - 5], [-14, 2, 0, 0]
+    pv = P.PlaintextVector.from_ints(sigs, exps)
+    b = wire.plaintext_vector_to_bincode(pv)
+    assert b == ct_vec_bytes(sigs, exps)
+    assert wire.plaintext_vector_from_bincode(b).to_ints() == (sigs, exps)
