@@ -122,23 +122,38 @@ def pmc_traffic_per_elem():
     return float(d["hbm_bytes_per_elem"]), os.path.relpath(paths[-1], ROOT)
 
 
-def cpu_baseline(p: int, q: int, seconds: float = 12.0):
-    """libgmp restatement of the reference's per-element encrypt (oracle/gmp_ref.c)."""
-    from oracle import gmp_ref
-    key = gmp_ref.GmpKey(p * q, p, q)
-    t1 = key.bench("encrypt", 20, 1)
-    per1 = 20 / t1
-    threads = int(os.environ.get("FPHE_CPU_THREADS", "16"))
-    per_thread = max(8, int(per1 * seconds))
-    tw = key.bench("encrypt", per_thread, threads)
+def cpu_baseline(p: int, q: int, seconds: float = 3.0):
+    """The libgmp restatement of the reference's per-element call sequence (oracle/gmp_ref.c)
+    timed the way FATE runs it: one worker process per core (oracle/cpu_baseline.py), for
+    encrypt (the headline), decrypt and ct-add.  Runs as a child process: its forked
+    workers must not inherit this GPU-initialised process."""
+    import subprocess
+    procs = int(os.environ.get("FPHE_CPU_PROCS", "0"))
+    cmd = [sys.executable, "-m", "oracle.cpu_baseline", "--p", hex(p), "--q", hex(q), "--seconds", str(seconds)]
+    if procs:
+        cmd += ["--procs", str(procs)]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        raise RuntimeError(r.stderr.strip()[-300:])
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    ops = d["ops"]
     return {
-        "value": round(per_thread * threads / tw, 2),
+        "value": ops["encrypt"]["per_s"],
         "unit": "encrypts/s",
-        "cores": threads,
+        "cores": d["procs"],
         "kind": "port",
-        "per_core": round(per1, 2),
-        "sample": f"{per_thread * threads} Paillier-2048 obfuscated encryptions ({per_thread}/thread x {threads} "
-                  f"pthreads) through libgmp mpz_powm/mul/tdiv_r in the reference's call order (oracle/gmp_ref.c)",
+        "per_core": ops["encrypt"]["per_core_per_s"],
+        "decrypt_per_s": ops["decrypt"]["per_s"],
+        "ct_add_per_s": ops["add"]["per_s"],
+        "ct_add_hetero_lr_gaps_per_s": ops["add_gap"]["per_s"],
+        "cpu_model": d["cpu_model"],
+        "machine_cores": d["machine_cores"],
+        "usable_cores": d["usable_cores"],
+        "sample": (f"{d['procs']} worker processes (one per core, FATE's process pool), libgmp mpz_* in the "
+                   f"reference's call order (oracle/gmp_ref.c), 2048-bit key: {ops['encrypt']['elements']} "
+                   f"obfuscated encryptions, {ops['decrypt']['elements']} CRT decryptions, "
+                   f"{ops['add']['elements']} aligned ct-adds (mpz_mul + tdiv_r), {ops['add_gap']['elements']} ct-adds "
+                   f"with the Hetero-LR exponent-gap mix (+ mpz_powm by 16^gap)"),
     }
 
 
@@ -229,20 +244,43 @@ def hetero_lr_leg(P, pk, sk, coder, N, F, rank, dev):
             "gradient_allclose": bool(torch.allclose(got, want, rtol=1e-9, atol=1e-9))}
 
 
+def launch_ranks(nproc: int) -> int:
+    """`bench.py --gpus N` (N > 1) started without a launcher: run the same command line as N
+    ranks under torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1) and
+    return its exit code.  Called before anything touches the GPU; the ranks are child
+    processes, not an exec of this one."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--n", "--elements", type=int, default=1 << 20, dest="n", help="elements per GPU")
+    ap.add_argument("--total", type=int, default=0,
+                    help="BASELINE config 5: this many elements in all, split over the ranks (strong "
+                         "scaling), then the ciphertext all-gather; replaces --n")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip decrypt/add/e2e legs")
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the ciphertext all-gather leg")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)")
     dist = world > 1
     if dist:
         import torch.distributed as tdist
@@ -269,10 +307,17 @@ def main() -> None:
     pk_kh = P.keypair_from_primes(p, q, keyholder=True)[1]
     key_bits = pk.n.bit_length()
 
-    N = args.n
-    g = torch.Generator().manual_seed(20241218 + rank)
+    strong = args.total > 0
+    if strong:
+        # BASELINE config 5: contiguous tile-aligned shards of one vector (fate_amd.dist)
+        from fate_amd.dist import shard_bounds
+        s0, s1 = shard_bounds(args.total, rank, world)
+        N, seed = s1 - s0, 20241218 + s0
+    else:
+        N, seed = args.n, 20241218 + rank
+    g = torch.Generator().manual_seed(seed)
     x = torch.randn(N, generator=g, dtype=torch.float32) * 4
-    x[:8] = torch.tensor([0.0, -0.0, 1e-30, -1e-30, 3.4e38, -3.4e38, 1.0, -1.0])
+    x[:8] = torch.tensor([0.0, -0.0, 1e-30, -1e-30, 3.4e38, -3.4e38, 1.0, -1.0])[:N]
     xd = x.to(dev)
     stream = torch.cuda.current_stream(dev)
 
@@ -309,7 +354,7 @@ def main() -> None:
         tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
         elapsed = float(tt.item())
     enc_kernel_ms = sum(a.elapsed_time(b) for a, b in ev_enc) / max(len(ev_enc), 1)
-    value = world * N * args.steps / elapsed
+    value = (args.total if strong else world * N) * args.steps / elapsed
 
     # BASELINE config 5's exchange step, outside the timed region: every rank's ciphertext
     # shard all-gathered over RCCL/xGMI (fate_amd.dist.gather_tiles), so the whole vector
@@ -319,7 +364,8 @@ def main() -> None:
         from fate_amd.dist import gather_tiles
         barrier()
         tg = time.perf_counter()
-        Cg, sg, eg, total = gather_tiles(ct.C, ct.sign, ct.exp, ct.count)
+        Cg, sg, eg, counts = gather_tiles(ct.C, ct.sign, ct.exp, ct.count, trim=False)
+        total = sum(counts)
         barrier()
         gs = time.perf_counter() - tg
         tt = torch.tensor([gs], dtype=torch.float64, device=dev)
@@ -331,12 +377,13 @@ def main() -> None:
         gather_info = {
             "allgather": {"seconds": round(gs, 4), "elements": int(total), "bytes_per_elem": per_elem,
                           "recv_GBps_per_rank": round(recv / gs / 1e9, 2),
-                          "encrypt_plus_allgather_per_s": round(world * N / (elapsed / args.steps + gs), 1)},
+                          "encrypt_plus_allgather_per_s": round((args.total if strong else world * N)
+                                                                / (elapsed / args.steps + gs), 1)},
         }
         del Cg, sg, eg
 
     extras = {}
-    if not args.no_extras:
+    if not args.no_extras and not strong:
         # decrypt (device-resident), with the bit-exact round trip check
         torch.cuda.synchronize(dev)
         e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
@@ -508,26 +555,25 @@ def main() -> None:
     achieved = mac_launch / (enc_kernel_ms / 1e3) / 1e12
     # algorithmic HBM bytes per element: f32 sig/exp/neg read (13 B) + C (512 B) + sign (1 B) written
     hbm_bytes = N * (8 + 1 + 4 + key_bits // 4 + 1)
-    r27 = os.environ.get("FPHE_ENGINE", "27") != "32"
     mad27 = N * enc_mad27_per_elem(key_bits, pk.n) / (enc_kernel_ms / 1e3) / 1e12
     tb, tsrc = pmc_traffic_per_elem()
     roofline = {
         "bound": "valu",
-        "kernel": "k_encrypt27<128,6> (+k_draw_r)" if r27 else "k_encrypt2<128,5> (+k_draw_r)",
+        "kernel": "k_encrypt27<128,6> (+k_draw_r)",
         "achieved": round(achieved, 3),
         "peak": round(PEAK_TMAC32, 3),
         "unit": "TMAC32/s",
         "frac": round(achieved / PEAK_TMAC32, 4),
         # HBM bytes per launch from PMC counters (separate --pmc runs, calibrated; dominated
         # by the window-table scratch, see the profile's note); None if not profiled
-        "traffic": round(tb * N) if (tb is not None and r27) else None,
-        "traffic_source": tsrc if r27 else None,
+        "traffic": round(tb * N) if tb is not None else None,
+        "traffic_source": tsrc,
         "per_elem_mac32": enc_mac32_per_elem(key_bits),
         "kernel_ms": round(enc_kernel_ms, 3),
         # instruction-issue view of the same launch: 27-bit-limb MACs issued (one
         # v_mad_u64_u32 each) against the same half-rate mad peak
         "issue": {"mad64_per_elem": enc_mad27_per_elem(key_bits, pk.n), "achieved": round(mad27, 3),
-                  "peak": round(PEAK_TMAC32, 3), "unit": "Tmad/s", "frac": round(mad27 / PEAK_TMAC32, 4)} if r27 else None,
+                  "peak": round(PEAK_TMAC32, 3), "unit": "Tmad/s", "frac": round(mad27 / PEAK_TMAC32, 4)},
         "hbm": {"achieved": round(hbm_bytes / (enc_kernel_ms / 1e3) / 1e9, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s"},
     }
     out = {
@@ -539,17 +585,20 @@ def main() -> None:
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic",
-        "config": {"workload": "paillier2048_encrypt_f32_1M", "key_bits": key_bits, "elements_per_gpu": N,
-                   "obfuscate": True, "parallelism": f"shard{world}"},
+        "config": ({"workload": f"paillier2048_encrypt_f32_{args.total}_strong", "key_bits": key_bits,
+                    "elements_total": args.total, "elements_rank0": N, "obfuscate": True,
+                    "parallelism": f"shard{world}"} if strong else
+                   {"workload": "paillier2048_encrypt_f32_1M", "key_bits": key_bits, "elements_per_gpu": N,
+                    "obfuscate": True, "parallelism": f"shard{world}"}),
         "roofline": roofline,
     }
     out.update(gather_info)
     out.update(extras)
-    if world == 1 and not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline and not strong:
         try:
             out["cpu_baseline"] = cpu_baseline(p, q)
         except Exception as exc:  # GMP missing on the box: say so, do not fake a number

@@ -33,9 +33,9 @@ EXPORTED_SYMBOLS = (
     "fphe_ctx_create", "fphe_ctx_destroy", "fphe_ctx_limbs",
     "fphe_encode_f32", "fphe_encode_f64", "fphe_decode_f32", "fphe_decode_f64",
     "fphe_encode_i64", "fphe_decode_i64", "fphe_decode_i32", "fphe_pack_f64", "fphe_unpack_f64",
-    "fphe_encrypt", "fphe_encrypt_crt", "fphe_decrypt", "fphe_add", "fphe_mul", "fphe_neg", "fphe_sqmul",
+    "fphe_encrypt", "fphe_encrypt_crt", "fphe_decrypt", "fphe_add", "fphe_add_ordered", "fphe_mul", "fphe_neg", "fphe_sqmul",
     "fphe_fold", "fphe_permute", "fphe_export_signed", "fphe_import_signed",
-    "fphe_wire_lengths", "fphe_wire_encode", "fphe_wire_scan", "fphe_wire_decode",
+    "fphe_wire_lengths", "fphe_wire_encode", "fphe_wire_scan", "fphe_wire_decode", "fphe_chacha20_blocks",
 )
 
 _lock = threading.Lock()
@@ -96,6 +96,9 @@ def load() -> ctypes.CDLL:
         lib.fphe_decrypt.restype = st
         lib.fphe_add.argtypes = [vp, vp, vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_size_t, vp, vp, vp, vp]
         lib.fphe_add.restype = st
+        lib.fphe_add_ordered.argtypes = [vp, vp, vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_size_t, vp, vp, vp, vp,
+                                         vp]
+        lib.fphe_add_ordered.restype = st
         lib.fphe_mul.argtypes = [vp, vp, vp, vp, vp, ctypes.c_uint32, vp, vp, ctypes.c_int, ctypes.c_size_t,
                                  vp, vp, vp, vp, vp]
         lib.fphe_mul.restype = st
@@ -112,6 +115,8 @@ def load() -> ctypes.CDLL:
             getattr(lib, name).argtypes = [vp, vp, vp, ctypes.c_size_t, vp, vp, vp]
             getattr(lib, name).restype = st
         sz = ctypes.c_size_t
+        lib.fphe_chacha20_blocks.argtypes = [vp, ctypes.c_uint32, vp, sz, vp, vp]
+        lib.fphe_chacha20_blocks.restype = st
         lib.fphe_wire_lengths.argtypes = [vp, vp, ctypes.c_uint32, sz, vp, vp]
         lib.fphe_wire_encode.argtypes = [vp, vp, vp, ctypes.c_uint32, sz, vp, vp, vp, vp]
         lib.fphe_wire_scan.argtypes = [vp, sz, sz, sz, vp, vp, vp, vp, vp, vp]

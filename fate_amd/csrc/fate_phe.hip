@@ -2,8 +2,9 @@
 //
 // Reference semantics: rust/fate_utils/crates/paillier/src/lib.rs (L0) and
 // rust/fate_utils/crates/fixedpoint_paillier/src/lib.rs (L1); SURVEY.md Appendix A.
-// Every kernel processes one element per lane (TPI = 1) with a grid-stride loop over
-// 64-element wave groups; see DESIGN.md for the layout and roofline of each kernel.
+// The modexp kernels (kernels27.h) spread an element over TPI adjacent lanes (27-bit limbs);
+// the codec, CRT-tail, permutation and wire kernels take one element per lane.  All run
+// grid-stride loops over 64-element tiles; see DESIGN.md for layouts and rooflines.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -14,7 +15,6 @@
 
 #include "../../include/fate_phe.h"
 #include "mont_dev.h"
-#include "mont2_dev.h"
 #include "chacha_dev.h"
 #include "host_bn.h"
 
@@ -24,7 +24,6 @@ namespace {
 
 constexpr int kBlock = 256;      // 4 waves per workgroup
 constexpr int kWavesPerBlock = kBlock / FPHE_WAVE;
-constexpr int kWinEnc = 5;       // window of the 32-bit engine's shared-exponent modexps (r^n, c^(p-1))
 constexpr int kWinSlide = 6;     // sliding window of the 27-bit engine's shared-exponent modexps
 constexpr int kWinMul = 4;       // window of the per-lane-exponent modexp (ct x pt)
 
@@ -153,7 +152,10 @@ __device__ __forceinline__ void draw_r(u32 (&A)[L1], const KeyArgs& K, const Cha
 #pragma unroll
       for (int b = 0; b < NB; ++b) {
         u32 blk[16];
-        chacha20_block(ck, attempt * NB + b, (u32)e, (u32)(nonce >> 32), (u32)nonce, blk);
+        // element index: low 32 bits in the first nonce word, bits 32..47 in the top half
+        // of the block counter (attempt * NB + b stays far below 2^16)
+        chacha20_block(ck, (attempt * NB + b) | ((u32)(e >> 32) << 16), (u32)e, (u32)(nonce >> 32), (u32)nonce,
+                       blk);
 #pragma unroll
         for (int i = 0; i < 16; ++i)
           if (b * 16 + i < L1) x[b * 16 + i] = blk[i];
@@ -181,59 +183,19 @@ __device__ __forceinline__ void draw_r(u32 (&A)[L1], const KeyArgs& K, const Cha
   }
 }
 
-template <int L, int W>
-__global__ __launch_bounds__(kBlock) void k_encrypt(KeyArgs K, const u32* __restrict__ P, u32 lp,
-                                                    const u8* __restrict__ neg, u32 ntiles, int obf,
-                                                    const u32* __restrict__ rin, ChaChaKey ck, u64 nonce,
-                                                    u32* __restrict__ Cout, u8* __restrict__ sout,
-                                                    u32* __restrict__ scratch) {
-  constexpr int L1 = L / 2;
-  extern __shared__ __attribute__((aligned(16))) u32 lds[];
-  const WaveCtx w = wave_ctx();
-  u32* slot = lds_slot<L>(lds, w.lane);
-  const Tile tb = make_tile(scratch + (size_t)w.gw * ((size_t)(1 << W) * L * FPHE_WAVE), (1u << W) * L * 256u, w.lane);
-  for (u32 tile = w.gw; tile < ntiles; tile += w.nw) {
-    const size_t e = (size_t)tile * FPHE_WAVE + w.lane;
-    const Tile Pt = make_tile(P + (size_t)tile * lp * FPHE_WAVE, lp * 256u, w.lane);
-    const Tile Ct = make_tile(Cout + (size_t)tile * L * FPHE_WAVE, L * 256u, w.lane);
-    const bool mneg = nude_to_slot<L>(slot, K, Pt, lp, neg[e] != 0);
-    if (!obf) {
-#pragma unroll
-      for (int j = 0; j < L; ++j) Ct.st(slot[j * FPHE_WAVE], j * 256u);
-      sout[e] = mneg ? 1 : 0;
-      continue;
-    }
-    // stash C_nude in table entry 0 (powm_uniform uses entries 1 .. 2^W-1)
-#pragma unroll
-    for (int j = 0; j < L; ++j) tb.st(slot[j * FPHE_WAVE], j * 256u);
-    u32 A[L];
-    if (rin) {
-      const Tile Rt = make_tile(rin + (size_t)tile * L1 * FPHE_WAVE, L1 * 256u, w.lane);
-#pragma unroll
-      for (int j = 0; j < L1; ++j) A[j] = Rt.ld(j * 256u);
-#pragma unroll
-      for (int j = L1; j < L; ++j) A[j] = 0;
-    } else {
-      u32 r[L1];
-      draw_r<L1>(r, K, ck, nonce, e);
-#pragma unroll
-      for (int j = 0; j < L1; ++j) A[j] = r[j];
-#pragma unroll
-      for (int j = L1; j < L; ++j) A[j] = 0;
-    }
-    slot_store_uniform<L>(slot, K.N2_R2);
-    mont_mul<L>(A, slot, K.N2, K.n2_n0inv);                           // r R
-    powm_uniform<L, W>(A, slot, tb, K.N2, K.n2_n0inv, K.n, K.nbits);  // r^n R
-    tile_to_slot<L>(slot, tb, 0u);
-    mont_mul<L>(A, slot, K.N2, K.n2_n0inv);                           // r^n * C_nude
-    tile_store<L>(Ct, 0u, A);
-    sout[e] = mneg ? 1 : 0;
-  }
-}
-
 // r for every element into a tile-major [ntiles][L1][64] buffer (ChaCha20 per element,
 // rejection sampling into [1, n-1]); kept out of the modexp kernel so its registers do
 // not count against the modexp's occupancy.
+__global__ __launch_bounds__(256) void k_chacha_blocks(ChaChaKey ck, u32 counter, u32 n0, u32 n1, u32 n2,
+                                                       size_t nblocks, u32* __restrict__ out) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nblocks; i += (size_t)gridDim.x * blockDim.x) {
+    u32 blk[16];
+    chacha20_block(ck, counter + (u32)i, n0, n1, n2, blk);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) out[i * 16 + k] = blk[k];
+  }
+}
+
 template <int L1>
 __global__ __launch_bounds__(256) void k_draw_r(KeyArgs K, size_t count, ChaChaKey ck, u64 nonce, u32* __restrict__ R) {
   for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < count; e += (size_t)gridDim.x * blockDim.x) {
@@ -241,61 +203,6 @@ __global__ __launch_bounds__(256) void k_draw_r(KeyArgs K, size_t count, ChaChaK
     draw_r<L1>(r, K, ck, nonce, e);
 #pragma unroll
     for (int j = 0; j < L1; ++j) R[tiled(e, L1, j)] = r[j];
-  }
-}
-
-// Two lanes per element (mont2_dev.h) for 4096-bit n^2: lanes e / e+32 of a wave hold the
-// low / high 64 limbs of one element; a wave covers 32 elements (half a memory tile).
-template <int L, int W>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_encrypt2(KeyArgs K, const u32* __restrict__ P, u32 lp,
-                                                     const u8* __restrict__ neg, size_t count, int obf,
-                                                     const u32* __restrict__ rin, u32* __restrict__ Cout,
-                                                     u8* __restrict__ sout, u32* __restrict__ scratch) {
-  constexpr int LL = L / 2;  // limbs per lane (== limbs of n)
-  extern __shared__ __attribute__((aligned(16))) u32 lds[];
-  const WaveCtx w = wave_ctx();
-  const int e = w.lane & 31, h = w.lane >> 5;
-  const u32 wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  u32* bcol = lds + wib * (L * kHalf) + e;
-  const u32 hoff = half_off<LL>(h);
-  const Tile tb = make_tile(scratch + (size_t)w.gw * ((size_t)(1 << W) * LL * FPHE_WAVE), (1u << W) * LL * 256u, w.lane);
-  u32 NV[LL];
-#pragma unroll
-  for (int j = 0; j < LL; ++j) NV[j] = K.N2[h * LL + j];
-  const u32 nwt = (u32)((count + kHalf - 1) / kHalf);
-  for (u32 wt = w.gw; wt < nwt; wt += w.nw) {
-    const u32 tile = wt >> 1;
-    const u32 col = (wt & 1u) * kHalf + (u32)e;
-    const size_t elem = (size_t)tile * FPHE_WAVE + col;
-    Tile Pt = make_tile(P + (size_t)tile * lp * FPHE_WAVE, lp * 256u, 0);
-    Pt.vo = col * 4u;
-    Tile Ct = make_tile(Cout + (size_t)tile * L * FPHE_WAVE, L * 256u, 0);
-    Ct.vo = ((u32)h * LL * FPHE_WAVE + col) * 4u;
-    bool mneg = false;
-    if (h == 0) mneg = nude_to_slot<L, kHalf>(bcol, K, Pt, lp, neg[elem] != 0);
-    if (!obf) {
-#pragma unroll
-      for (int j = 0; j < LL; ++j) Ct.st(bcol[hoff + j * kHalf], j * 256u);
-      if (h == 0) sout[elem] = mneg ? 1 : 0;
-      continue;
-    }
-    slot2_to_tile<LL>(tb, 0u, bcol, hoff);  // stash this lane's half of C_nude in table entry 0
-    // r: injected, or drawn beforehand into the same buffer by k_draw_r (launch_encrypt)
-    u32 A[LL];
-    {
-      Tile Rt = make_tile(rin + (size_t)tile * LL * FPHE_WAVE, LL * 256u, 0);
-      Rt.vo = col * 4u;
-#pragma unroll
-      for (int j = 0; j < LL; ++j) A[j] = h == 0 ? Rt.ld(j * 256u) : 0u;
-    }
-    slot2_store_uniform<LL>(bcol, K.N2_R2, hoff, h);
-    mont_mul2<LL>(A, bcol, NV, K.n2_n0inv);                                   // r R
-    powm_uniform2<LL, W>(A, bcol, tb, NV, K.n2_n0inv, K.n, K.nbits, hoff);  // r^n R
-    tile2_to_slot<LL>(bcol, tb, 0u, hoff);
-    mont_mul2<LL>(A, bcol, NV, K.n2_n0inv);                                   // r^n * C_nude
-#pragma unroll
-    for (int j = 0; j < LL; ++j) Ct.st(A[j], j * 256u);
-    if (h == 0) sout[elem] = mneg ? 1 : 0;
   }
 }
 
@@ -342,55 +249,6 @@ __device__ __forceinline__ void crt_tail(u32 (&dout)[L / 4], const u32 (&A)[L / 
   mont_mul<LQ>(Ls, slot, S, s_n0inv);  // L * h_s mod s
 #pragma unroll
   for (int j = 0; j < LQ; ++j) dout[j] = Ls[j];
-}
-
-// d_s = L_s(c^(s-1) mod s^2) * h_s mod s  for s in {p, q}
-template <int L, int W>
-__device__ __forceinline__ void crt_half(u32 (&dout)[L / 4], const Tile& Cin, u32* slot, const Tile& tb,
-                                         const u32* __restrict__ S2, u32 s2_n0inv, const u32* __restrict__ S2_R3,
-                                         const u32* __restrict__ sm1, int sm1_bits, const u32* __restrict__ S,
-                                         u32 s_n0inv, const u32* __restrict__ sinv2, const u32* __restrict__ hsR) {
-  constexpr int LH = L / 2;
-  u32 A[LH];
-  {
-    // REDC of the 2LH-limb c modulo S2 (c < n^2 < S2 * 2^(32 LH))
-    u32 T[L + 1];
-#pragma unroll
-    for (int j = 0; j < L; ++j) T[j] = Cin.ld(j * 256u);
-    T[L] = 0;
-#pragma unroll 1
-    for (int i = 0; i < LH; ++i) {
-      const u32 m = T[0] * s2_n0inv;
-      u64 acc = (u64)m * S2[0] + T[0];
-#pragma unroll
-      for (int j = 1; j < LH; ++j) {
-        acc = (u64)m * S2[j] + T[j] + (acc >> 32);
-        T[j - 1] = (u32)acc;
-      }
-#pragma unroll
-      for (int j = LH; j <= L; ++j) {
-        acc = (u64)T[j] + (acc >> 32);
-        T[j - 1] = (u32)acc;
-      }
-      T[L] = (u32)(acc >> 32);
-    }
-    u32 br = 0;
-#pragma unroll
-    for (int j = 0; j < LH; ++j) {
-      const u64 d = (u64)T[j] - S2[j] - br;
-      A[j] = (u32)d;
-      br = (u32)(d >> 63);
-    }
-    const bool keep = (T[LH] == 0) & (br != 0);
-#pragma unroll
-    for (int j = 0; j < LH; ++j) A[j] = keep ? T[j] : A[j];
-  }
-  slot_store_uniform<LH>(slot, S2_R3);
-  mont_mul<LH>(A, slot, S2, s2_n0inv);                            // c R mod s^2
-  powm_uniform<LH, W>(A, slot, tb, S2, s2_n0inv, sm1, sm1_bits);  // c^(s-1) R
-  slot_store_small<LH>(slot, 1u);
-  mont_mul<LH>(A, slot, S2, s2_n0inv);                            // y = c^(s-1) mod s^2
-  crt_tail<L>(dout, A, slot, S, s_n0inv, sinv2, hsR);
 }
 
 // m = dp + p * ((dq - dp) p^{-1} mod q): paillier/src/lib.rs:163-172
@@ -443,24 +301,6 @@ __device__ __forceinline__ void crt_combine(const u32 (&dp)[L / 4], const u32 (&
   for (int j = 0; j < LQ; ++j) Pt.st(T[j], (u32)(LQ + j) * 256u);
 }
 
-template <int L, int W>
-__global__ __launch_bounds__(kBlock) void k_decrypt(KeyArgs K, const u32* __restrict__ C, u32 ntiles,
-                                                    u32* __restrict__ Pout, u32* __restrict__ scratch) {
-  constexpr int LH = L / 2, LQ = L / 4;
-  extern __shared__ __attribute__((aligned(16))) u32 lds[];
-  const WaveCtx w = wave_ctx();
-  u32* slot = lds_slot<LH>(lds, w.lane);
-  const Tile tb = make_tile(scratch + (size_t)w.gw * ((size_t)(1 << W) * LH * FPHE_WAVE), (1u << W) * LH * 256u, w.lane);
-  for (u32 tile = w.gw; tile < ntiles; tile += w.nw) {
-    const Tile Cin = make_tile(C + (size_t)tile * L * FPHE_WAVE, L * 256u, w.lane);
-    const Tile Pt = make_tile(Pout + (size_t)tile * LH * FPHE_WAVE, LH * 256u, w.lane);
-    u32 dp[LQ], dq[LQ];
-    crt_half<L, W>(dp, Cin, slot, tb, K.P2, K.p2_n0inv, K.P2_R3, K.pm1, K.pm1_bits, K.p, K.p_n0inv, K.pinv2, K.hpR);
-    crt_half<L, W>(dq, Cin, slot, tb, K.Q2, K.q2_n0inv, K.Q2_R3, K.qm1, K.qm1_bits, K.q, K.q_n0inv, K.qinv2, K.hqR);
-    crt_combine<L>(dp, dq, K, slot, Pt);
-  }
-}
-
 // decrypt, CRT phase for the reduced-radix path: y_p, y_q (k_pow_half27<., ., false>) -> m.
 template <int L>
 __global__ __launch_bounds__(kBlock) void k_decrypt_crt(KeyArgs K, const u32* __restrict__ Y, u32 ntiles,
@@ -484,174 +324,6 @@ __global__ __launch_bounds__(kBlock) void k_decrypt_crt(KeyArgs K, const u32* __
       crt_tail<L>(dq, A, slot, K.q, K.q_n0inv, K.qinv2, K.hqR);
     }
     crt_combine<L>(dp, dq, K, slot, Pt);
-  }
-}
-
-// ======================================================================================
-// add: Ciphertext::add (fixedpoint_paillier/src/lib.rs:301-333) with decrese_exp_to
-// (:250-258): the higher-exp operand x is raised to 16^d = 2^(4d) (4d Montgomery
-// squarings), then multiplied into y; sign = XOR of the operands at the final product.
-// ======================================================================================
-template <int L>
-__global__ __launch_bounds__(kBlock) void k_add(KeyArgs K, const u32* __restrict__ Ca, const u8* __restrict__ sa,
-                                                const int32_t* __restrict__ ea, const u32* __restrict__ Cb,
-                                                const u8* __restrict__ sb, const int32_t* __restrict__ eb,
-                                                int bstride, u32 ntiles, u32* __restrict__ Co,
-                                                u8* __restrict__ so, int32_t* __restrict__ eo) {
-  extern __shared__ __attribute__((aligned(16))) u32 lds[];
-  const WaveCtx w = wave_ctx();
-  u32* slot = lds_slot<L>(lds, w.lane);
-  for (u32 tile = w.gw; tile < ntiles; tile += w.nw) {
-    const size_t e = (size_t)tile * FPHE_WAVE + w.lane;
-    const size_t be = bstride ? e : 0;
-    const Tile At = make_tile(Ca + (size_t)tile * L * FPHE_WAVE, L * 256u, w.lane);
-    const Tile Bt = bstride ? make_tile(Cb + (size_t)tile * L * FPHE_WAVE, L * 256u, w.lane)
-                            : make_tile(Cb, L * 256u, 0);
-    const Tile Ot = make_tile(Co + (size_t)tile * L * FPHE_WAVE, L * 256u, w.lane);
-    const int xa = ea[e], xb = eb[be];
-    const u32 sav = sa[e], sbv = sb[be];
-    const bool x_is_a = xa > xb;
-    u32 A[L];
-    u32 ra = 0, rb = 0;
-#pragma unroll
-    for (int j = 0; j < L; ++j) {
-      const u32 va = At.ld(j * 256u), vb = Bt.ld(j * 256u);
-      ra |= j == 0 ? (va ^ 1u) : va;
-      rb |= j == 0 ? (vb ^ 1u) : vb;
-      A[j] = x_is_a ? va : vb;
-    }
-    // literal-1 tests (:303-308): the signed integer equals 1 iff sign == 0 and C == 1
-    const bool lit_a = (ra == 0) && (sav == 0);
-    const bool lit_b = (rb == 0) && (sbv == 0);
-    int d = x_is_a ? xa - xb : xb - xa;
-    if (lit_a || lit_b) d = 0;
-    slot_store_uniform<L>(slot, K.N2_R2);
-    mont_mul<L>(A, slot, K.N2, K.n2_n0inv);  // x R
-    const int nsq = wave_max_int(4 * d);
-#pragma unroll 1
-    for (int k = 0; k < nsq; ++k) {
-      if (k < 4 * d) mont_sqr<L>(A, slot, K.N2, K.n2_n0inv);
-    }
-#pragma unroll
-    for (int j = 0; j < L; ++j) {
-      const u32 va = At.ld(j * 256u), vb = Bt.ld(j * 256u);
-      slot[j * FPHE_WAVE] = x_is_a ? vb : va;
-    }
-    mont_mul<L>(A, slot, K.N2, K.n2_n0inv);  // x^(16^d) * y mod n^2
-    const u32 sy = x_is_a ? sbv : sav;
-    u32 sign = d == 0 ? (sav ^ sbv) : sy;
-    int exo = xa < xb ? xa : xb;
-    if (lit_a || lit_b) {
-#pragma unroll
-      for (int j = 0; j < L; ++j) {
-        const u32 va = At.ld(j * 256u), vb = Bt.ld(j * 256u);
-        A[j] = lit_a ? vb : va;
-      }
-      sign = lit_a ? sbv : sav;
-      exo = lit_a ? xb : xa;
-    }
-    tile_store<L>(Ot, 0u, A);
-    so[e] = (u8)sign;
-    eo[e] = exo;
-  }
-}
-
-// ======================================================================================
-// mul: Ciphertext::mul (fixedpoint_paillier/src/lib.rs:334-349): c^b mod n^2 with a
-// per-lane exponent b (fixed window over the wave's longest exponent), exp = e_c + e_b.
-// ======================================================================================
-template <int L, int W>
-__global__ __launch_bounds__(kBlock) void k_mul(KeyArgs K, const u32* __restrict__ Ca, const u8* __restrict__ sa,
-                                                const int32_t* __restrict__ ea, const u32* __restrict__ P, u32 lp,
-                                                const u8* __restrict__ pneg, const int32_t* __restrict__ pexp,
-                                                int pstride, size_t count, u32* __restrict__ Co,
-                                                u8* __restrict__ so, int32_t* __restrict__ eo,
-                                                int32_t* __restrict__ err, u32* __restrict__ scratch) {
-  const u32 ntiles = (u32)((count + FPHE_WAVE - 1) / FPHE_WAVE);
-  constexpr int L1 = L / 2;
-  constexpr u32 TE = L * 256u;
-  extern __shared__ __attribute__((aligned(16))) u32 lds[];
-  const WaveCtx w = wave_ctx();
-  u32* slot = lds_slot<L>(lds, w.lane);
-  const Tile tb = make_tile(scratch + (size_t)w.gw * ((size_t)(1 << W) * L * FPHE_WAVE), (1u << W) * TE, w.lane);
-  for (u32 tile = w.gw; tile < ntiles; tile += w.nw) {
-    const size_t e = (size_t)tile * FPHE_WAVE + w.lane;
-    const size_t pe = pstride ? e : 0;
-    const Tile Pt = pstride ? make_tile(P + (size_t)tile * lp * FPHE_WAVE, lp * 256u, w.lane)
-                            : make_tile(P, lp * 256u, 0);
-    const Tile At = make_tile(Ca + (size_t)tile * L * FPHE_WAVE, L * 256u, w.lane);
-    const Tile Ot = make_tile(Co + (size_t)tile * L * FPHE_WAVE, L * 256u, w.lane);
-    // classify the plaintext significand (:335-344)
-    u32 any = 0;
-    int ebits = 0;
-    u32 br_max = 0, br_nmm = 0;  // borrows of max_int - P and P - n_mm
-#pragma unroll 4
-    for (int j = 0; j < L1; ++j) {
-      const u32 pj = (u32)j < lp ? Pt.ld((u32)j * 256u) : 0u;
-      any |= pj;
-      if (pj) ebits = 32 * j + 32 - __clz(pj);
-      const u64 d1 = (u64)K.max_int[j] - pj - br_max;
-      br_max = (u32)(d1 >> 63);
-      const u64 d2 = (u64)pj - K.n_mm[j] - br_nmm;
-      br_nmm = (u32)(d2 >> 63);
-    }
-    const bool isneg = (pneg[pe] != 0) && (any != 0);
-    const bool big = !isneg && (br_nmm == 0);              // P >= n - max_int
-    const bool invalid = !isneg && !big && (br_max != 0);  // P > max_int
-    u32 ef = 0;
-    if (isneg || big) ef |= FPHE_EF_NOT_INVERTIBLE;  // inverse branches: not yet on device
-    if (invalid) ef |= FPHE_EF_MUL_INVALID_PT;
-    if (e < count) set_err(err, ef);
-    if (isneg || big || invalid) ebits = 0;
-    const int maxbits = wave_max_int(ebits);
-    u32 A[L];
-    tile_load<L>(A, At, 0u);
-    slot_store_uniform<L>(slot, K.N2_R2);
-    mont_mul<L>(A, slot, K.N2, K.n2_n0inv);  // X = c R
-    if (maxbits > 0) {
-      slot_store<L>(slot, A);
-      tile_store<L>(tb, 1 * TE, A);
-#pragma unroll
-      for (int j = 0; j < L; ++j) tb.st(K.N2_R1[j], j * 256u);  // entry 0 = Montgomery 1
-#pragma unroll 1
-      for (int k = 2; k < (1 << W); ++k) {
-        mont_mul<L>(A, slot, K.N2, K.n2_n0inv);
-        tile_store<L>(tb, (u32)k * TE, A);
-      }
-      const int nwin = (maxbits + W - 1) / W;
-      auto digit = [&](int wi) -> u32 {
-        const int b0 = wi * W;
-        const u32 limb = (u32)(b0 >> 5);
-        const u32 v = limb < lp ? Pt.ld(limb * 256u) : 0u;
-        const u32 dd = (v >> (b0 & 31)) & ((1u << W) - 1);
-        return ebits == 0 ? 0u : dd;
-      };
-      // per-lane table entry: entry index differs by lane, so address it through the
-      // lane-varying voffset of the same (uniform) descriptor
-      auto entry_to = [&](u32 (&dst)[L], u32 dgt) {
-        Tile t = tb;
-        t.vo = tb.vo + dgt * TE;
-        tile_load<L>(dst, t, 0u);
-      };
-      entry_to(A, digit(nwin - 1));
-#pragma unroll 1
-      for (int wi = nwin - 2; wi >= 0; --wi) {
-#pragma unroll 1
-        for (int s = 0; s < W; ++s) mont_sqr<L>(A, slot, K.N2, K.n2_n0inv);
-        Tile t = tb;
-        t.vo = tb.vo + digit(wi) * TE;
-        tile_to_slot<L>(slot, t, 0u);
-        mont_mul<L>(A, slot, K.N2, K.n2_n0inv);
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < L; ++j) A[j] = K.N2_R1[j];
-    }
-    slot_store_small<L>(slot, 1u);
-    mont_mul<L>(A, slot, K.N2, K.n2_n0inv);  // leave Montgomery form
-    tile_store<L>(Ot, 0u, A);
-    so[e] = 0;
-    eo[e] = ea[e] + pexp[pe];
   }
 }
 
@@ -821,7 +493,6 @@ struct fphe_ctx {
   // two streams never share the window tables / intermediates at the same time
   hipStream_t scratch_stream = nullptr;
   bool scratch_used = false;
-  bool r27 = true;  // reduced-radix engine (FPHE_ENGINE=32 selects the 32-bit-limb kernels)
   std::mutex mu;
 };
 
@@ -902,95 +573,6 @@ int bpc_for_slot(int slot_limbs) {
 }  // namespace
 
 namespace {
-template <int L>
-fphe_status launch_encrypt(fphe_ctx* c, const uint32_t* P, uint32_t lp, const uint8_t* neg, size_t count,
-                                  int obf, const uint32_t* r, const uint32_t key[8], uint64_t nonce, uint32_t* C,
-                                  uint8_t* sign, hipStream_t s) {
-  if constexpr (L == 128) {  // two lanes per element: 2 waves/SIMD (VGPR), 2 workgroups/CU (64 KiB LDS each)
-    constexpr int LL = L / 2;
-    const size_t waves = (count + kHalf - 1) / kHalf;
-    size_t g = (size_t)c->cus * 2;
-    const size_t need = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
-    if (need < g) g = need;
-    const unsigned grid = (unsigned)(g ? g : 1);
-    const size_t lds = (size_t)kWavesPerBlock * L * kHalf * 4;
-    const size_t tbytes = (size_t)grid * kWavesPerBlock * (1u << kWinEnc) * LL * FPHE_WAVE * 4;
-    const size_t rbytes = (size_t)ntiles_of(count) * LL * FPHE_WAVE * 4;
-    if (ensure_scratch(c, tbytes + (r ? 0 : rbytes), s) != FPHE_OK) return FPHE_ERR_HIP;
-    const u32* rbuf = r;
-    if (obf && !r) {
-      u32* rdev = c->scratch + tbytes / 4;
-      ChaChaKey ck;
-      for (int i = 0; i < 8; ++i) ck.k[i] = key[i];
-      const unsigned rgrid = (unsigned)std::min<size_t>((count + 255) / 256, (size_t)c->cus * 4);
-      hipLaunchKernelGGL(k_draw_r<LL>, dim3(rgrid), dim3(256), 0, s, c->K, count, ck, nonce, rdev);
-      rbuf = rdev;
-    }
-    auto kern = k_encrypt2<L, kWinEnc>;
-    set_lds(kern, lds);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, P, lp, neg, count, obf, rbuf, C, sign,
-                       c->scratch);
-    return hip_ok(hipGetLastError());
-  }
-  const int bpc = bpc_for_slot(L);
-  const unsigned grid = grid_for(c, count, bpc);
-  const size_t lds = (size_t)kWavesPerBlock * L * FPHE_WAVE * 4;
-  const size_t sbytes = (size_t)grid * kWavesPerBlock * (1u << kWinEnc) * L * FPHE_WAVE * 4;
-  if (ensure_scratch(c, sbytes, s) != FPHE_OK) return FPHE_ERR_HIP;
-  ChaChaKey ck;
-  for (int i = 0; i < 8; ++i) ck.k[i] = key ? key[i] : 0u;
-  auto kern = k_encrypt<L, kWinEnc>;
-  set_lds(kern, lds);
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, P, lp, neg, ntiles_of(count), obf, r, ck, nonce, C,
-                     sign, c->scratch);
-  return hip_ok(hipGetLastError());
-}
-
-template <int L>
-fphe_status launch_decrypt(fphe_ctx* c, const uint32_t* C, size_t count, uint32_t* P, hipStream_t s) {
-  constexpr int LH = L / 2;
-  const int bpc = bpc_for_slot(LH);
-  const unsigned grid = grid_for(c, count, bpc);
-  const size_t lds = (size_t)kWavesPerBlock * LH * FPHE_WAVE * 4;
-  const size_t sbytes = (size_t)grid * kWavesPerBlock * (1u << kWinEnc) * LH * FPHE_WAVE * 4;
-  if (ensure_scratch(c, sbytes, s) != FPHE_OK) return FPHE_ERR_HIP;
-  auto kern = k_decrypt<L, kWinEnc>;
-  set_lds(kern, lds);
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, C, ntiles_of(count), P, c->scratch);
-  return hip_ok(hipGetLastError());
-}
-
-template <int L>
-fphe_status launch_add(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, const int32_t* ea,
-                              const uint32_t* Cb, const uint8_t* sb, const int32_t* eb, int bstride, size_t count,
-                              uint32_t* Co, uint8_t* so, int32_t* eo, hipStream_t s) {
-  const int bpc = bpc_for_slot(L);
-  const unsigned grid = grid_for(c, count, bpc);
-  const size_t lds = (size_t)kWavesPerBlock * L * FPHE_WAVE * 4;
-  auto kern = k_add<L>;
-  set_lds(kern, lds);
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, Ca, sa, ea, Cb, sb, eb, bstride, ntiles_of(count), Co,
-                     so, eo);
-  return hip_ok(hipGetLastError());
-}
-
-template <int L>
-fphe_status launch_mul(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, const int32_t* ea,
-                              const uint32_t* P, uint32_t lp, const uint8_t* pneg, const int32_t* pexp, int pstride,
-                              size_t count, uint32_t* Co, uint8_t* so, int32_t* eo, int32_t* err, hipStream_t s) {
-  const int bpc = bpc_for_slot(L);
-  const unsigned grid = grid_for(c, count, bpc);
-  const size_t lds = (size_t)kWavesPerBlock * L * FPHE_WAVE * 4;
-  const size_t sbytes = (size_t)grid * kWavesPerBlock * (1u << kWinMul) * L * FPHE_WAVE * 4;
-  if (ensure_scratch(c, sbytes, s) != FPHE_OK) return FPHE_ERR_HIP;
-  auto kern = k_mul<L, kWinMul>;
-  set_lds(kern, lds);
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, Ca, sa, ea, P, lp, pneg, pexp, pstride, count, Co,
-                     so, eo, err, c->scratch);
-  return hip_ok(hipGetLastError());
-}
-
-
 // ---- reduced-radix engine launchers (kernels27.h) ---------------------------------------
 template <int L>
 fphe_status launch_encrypt27(fphe_ctx* c, const uint32_t* P, uint32_t lp, const uint8_t* neg, size_t count, int obf,
@@ -1088,17 +670,30 @@ fphe_status launch_fold27(fphe_ctx* c, const uint32_t* Src, const uint8_t* ssign
   return hip_ok(hipGetLastError());
 }
 
+// Largest element count whose C vector (count x L words) one k_add27 launch addresses
+// through 32-bit buffer offsets (whole-vector descriptors, a margin below 4 GiB).
+size_t add_max_count(int L) {
+  return (((size_t)1 << 32) - ((size_t)1 << 20)) / ((size_t)L * 4) / FPHE_WAVE * FPHE_WAVE;
+}
+
 template <int L>
 fphe_status launch_add27(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, const int32_t* ea, const uint32_t* Cb,
-                         const uint8_t* sb, const int32_t* eb, int bstride, size_t count, uint32_t* Co, uint8_t* so,
-                         int32_t* eo, hipStream_t s) {
+                         const uint8_t* sb, const int32_t* eb, int bstride, size_t count, const int32_t* ord,
+                         uint32_t* Co, uint8_t* so, int32_t* eo, hipStream_t s) {
   constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = r27::LL * TPI;
   auto kern = k_add27<L>;
   const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
   set_lds(kern, lds);
-  const unsigned grid = occ_grid(c, kern, lds, (count + E - 1) / E);
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, Ca, sa, ea, Cb, sb, eb, bstride, count, Co, so, eo,
-                     (u32)NL);
+  const size_t cmax = add_max_count(L);
+  if (ord && count > cmax) return FPHE_ERR_ARG;  // an order must stay inside one addressable chunk
+  for (size_t s0 = 0; s0 < count; s0 += cmax) {  // whole tiles per chunk: pointer offsets stay tile-aligned
+    const size_t n = count - s0 < cmax ? count - s0 : cmax;
+    const size_t wo = s0 / FPHE_WAVE * L * FPHE_WAVE;  // word offset of the chunk's first tile
+    const unsigned grid = occ_grid(c, kern, lds, (n + E - 1) / E, "add27");
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, Ca + wo, sa + s0, ea + s0,
+                       bstride ? Cb + wo : Cb, bstride ? sb + s0 : sb, bstride ? eb + s0 : eb, bstride, n, ord,
+                       Co + wo, so + s0, eo + s0, (u32)NL);
+  }
   return hip_ok(hipGetLastError());
 }
 
@@ -1518,10 +1113,6 @@ fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, 
     K.Nn_27 = b + o_Nn_27; K.NnR1_27 = b + o_NnR1_27; K.NnR2_27 = b + o_NnR2_27;
     K.nn_np27 = hbn::neg_inv32(n[0]) & ((1u << 27) - 1u);
     K.nn_inv27 = (0u - hbn::neg_inv32(n[0])) & ((1u << 27) - 1u);
-    {
-      const char* eng = getenv("FPHE_ENGINE");
-      c->r27 = !(eng && strcmp(eng, "32") == 0);
-    }
     if (has_sk) {
       K.P2 = b + o_P2; K.P2_R3 = b + o_P2R3; K.pm1 = b + o_pm1; K.p = b + o_p; K.pinv2 = b + o_pinv2; K.hpR = b + o_hpR;
       K.Q2 = b + o_Q2; K.Q2_R3 = b + o_Q2R3; K.qm1 = b + o_qm1; K.q = b + o_q; K.qinv2 = b + o_qinv2; K.hqR = b + o_hqR;
@@ -1696,13 +1287,9 @@ fphe_status fphe_encrypt(fphe_ctx* c, const uint32_t* P, uint32_t lp, const uint
   if (obf && !r && !rng_key) return FPHE_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DevGuard g(c->device);
-  if (c->r27) {
-    if (c->L2 == 128)
-      return launch_encrypt27<128>(c, P, lp, neg, count, obf, r, rng_key, nonce, C, sign, (hipStream_t)stream);
-    return launch_encrypt27<64>(c, P, lp, neg, count, obf, r, rng_key, nonce, C, sign, (hipStream_t)stream);
-  }
-  if (c->L2 == 128) return launch_encrypt<128>(c, P, lp, neg, count, obf, r, rng_key, nonce, C, sign, (hipStream_t)stream);
-  return launch_encrypt<64>(c, P, lp, neg, count, obf, r, rng_key, nonce, C, sign, (hipStream_t)stream);
+  if (c->L2 == 128)
+    return launch_encrypt27<128>(c, P, lp, neg, count, obf, r, rng_key, nonce, C, sign, (hipStream_t)stream);
+  return launch_encrypt27<64>(c, P, lp, neg, count, obf, r, rng_key, nonce, C, sign, (hipStream_t)stream);
 }
 
 
@@ -1745,29 +1332,28 @@ fphe_status fphe_decrypt(fphe_ctx* c, const uint32_t* C, size_t count, uint32_t*
   if (!C || !P) return FPHE_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DevGuard g(c->device);
-  if (c->r27) {
-    if (c->L2 == 128) return launch_decrypt27<128>(c, C, count, P, (hipStream_t)stream);
-    return launch_decrypt27<64>(c, C, count, P, (hipStream_t)stream);
-  }
-  if (c->L2 == 128) return launch_decrypt<128>(c, C, count, P, (hipStream_t)stream);
-  return launch_decrypt<64>(c, C, count, P, (hipStream_t)stream);
+  if (c->L2 == 128) return launch_decrypt27<128>(c, C, count, P, (hipStream_t)stream);
+  return launch_decrypt27<64>(c, C, count, P, (hipStream_t)stream);
 }
 
 
-fphe_status fphe_add(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, const int32_t* ea, const uint32_t* Cb,
-                     const uint8_t* sb, const int32_t* eb, int b_stride, size_t count, uint32_t* Co, uint8_t* so,
-                     int32_t* eo, void* stream) {
+fphe_status fphe_add_ordered(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, const int32_t* ea,
+                             const uint32_t* Cb, const uint8_t* sb, const int32_t* eb, int b_stride, size_t count,
+                             const int32_t* order, uint32_t* Co, uint8_t* so, int32_t* eo, void* stream) {
   if (!c) return FPHE_ERR_ARG;
   if (count == 0) return FPHE_OK;
   if (!Ca || !sa || !ea || !Cb || !sb || !eb || !Co || !so || !eo) return FPHE_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DevGuard g(c->device);
-  if (c->r27) {
-    if (c->L2 == 128) return launch_add27<128>(c, Ca, sa, ea, Cb, sb, eb, b_stride, count, Co, so, eo, (hipStream_t)stream);
-    return launch_add27<64>(c, Ca, sa, ea, Cb, sb, eb, b_stride, count, Co, so, eo, (hipStream_t)stream);
-  }
-  if (c->L2 == 128) return launch_add<128>(c, Ca, sa, ea, Cb, sb, eb, b_stride, count, Co, so, eo, (hipStream_t)stream);
-  return launch_add<64>(c, Ca, sa, ea, Cb, sb, eb, b_stride, count, Co, so, eo, (hipStream_t)stream);
+  if (c->L2 == 128)
+    return launch_add27<128>(c, Ca, sa, ea, Cb, sb, eb, b_stride, count, order, Co, so, eo, (hipStream_t)stream);
+  return launch_add27<64>(c, Ca, sa, ea, Cb, sb, eb, b_stride, count, order, Co, so, eo, (hipStream_t)stream);
+}
+
+fphe_status fphe_add(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, const int32_t* ea, const uint32_t* Cb,
+                     const uint8_t* sb, const int32_t* eb, int b_stride, size_t count, uint32_t* Co, uint8_t* so,
+                     int32_t* eo, void* stream) {
+  return fphe_add_ordered(c, Ca, sa, ea, Cb, sb, eb, b_stride, count, nullptr, Co, so, eo, stream);
 }
 
 
@@ -1815,14 +1401,21 @@ fphe_status fphe_mul(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, const i
   if (!Ca || !sa || !ea || !P || !pneg || !pexp || !Co || !so || !eo || lp == 0) return FPHE_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DevGuard g(c->device);
-  if (c->r27) {
-    if (c->L2 == 128)
-      return launch_mul27<128>(c, Ca, sa, ea, P, lp, pneg, pexp, p_stride, count, Co, so, eo, err, (hipStream_t)stream);
-    return launch_mul27<64>(c, Ca, sa, ea, P, lp, pneg, pexp, p_stride, count, Co, so, eo, err, (hipStream_t)stream);
-  }
   if (c->L2 == 128)
-    return launch_mul<128>(c, Ca, sa, ea, P, lp, pneg, pexp, p_stride, count, Co, so, eo, err, (hipStream_t)stream);
-  return launch_mul<64>(c, Ca, sa, ea, P, lp, pneg, pexp, p_stride, count, Co, so, eo, err, (hipStream_t)stream);
+    return launch_mul27<128>(c, Ca, sa, ea, P, lp, pneg, pexp, p_stride, count, Co, so, eo, err, (hipStream_t)stream);
+  return launch_mul27<64>(c, Ca, sa, ea, P, lp, pneg, pexp, p_stride, count, Co, so, eo, err, (hipStream_t)stream);
+}
+
+fphe_status fphe_chacha20_blocks(const uint32_t key[8], uint32_t counter, const uint32_t nonce[3], size_t nblocks,
+                                 uint32_t* out, void* stream) {
+  if (!key || !nonce || (nblocks && !out)) return FPHE_ERR_ARG;
+  if (nblocks == 0) return FPHE_OK;
+  ChaChaKey ck;
+  for (int i = 0; i < 8; ++i) ck.k[i] = key[i];
+  const unsigned grid = (unsigned)std::min<size_t>((nblocks + 255) / 256, 1024);
+  hipLaunchKernelGGL(k_chacha_blocks, dim3(grid), dim3(256), 0, (hipStream_t)stream, ck, counter, nonce[0], nonce[1],
+                     nonce[2], nblocks, out);
+  return hip_ok(hipGetLastError());
 }
 
 fphe_status fphe_permute(const uint32_t* Cin, const uint8_t* sin, const int32_t* ein, uint32_t L,

@@ -16,14 +16,30 @@
 #define FPHE_ENC_OCC 3
 #endif
 #define FPHE_OCC2 __attribute__((amdgpu_waves_per_eu(2)))
-// ct-add / ct x pt / fold / squeeze stay at 2: a 3-wave build of k_add27<64> (88 VGPRs
-// spilled) raised an illegal memory access in the GPU parity test; not adopted, cause not
-// isolated (tools/clobcheck.py finds no clobber violation around the fused rows).
+// ct-add / ct x pt / squeeze run at 3 waves too (same-box A/B, profiles/r02/
+// r02f_ab_occ3_ops.txt: add +5%, ct x pt +1%); the segmented fold stays at 2 (-7% at 3).
+// Round 1's 3-wave k_add27<64> memory fault was the register allocator reusing a
+// per-lane buffer descriptor's VGPRs for a spill reload inside the readfirstlane loop
+// the compiler builds around such a load; the kernels no longer pick a
+// descriptor per lane, and tools/wfcheck.py checks every listing for such loops.
 #ifndef FPHE_MISC_OCC
-#define FPHE_MISC_OCC 2
+#define FPHE_MISC_OCC 3
+#endif
+#ifndef FPHE_FOLD_OCC
+#define FPHE_FOLD_OCC 2
 #endif
 #define FPHE_OCC_MISC __attribute__((amdgpu_waves_per_eu(FPHE_MISC_OCC)))
+#define FPHE_OCC_FOLD __attribute__((amdgpu_waves_per_eu(FPHE_FOLD_OCC)))
 #define FPHE_OCC_ENC __attribute__((amdgpu_waves_per_eu(FPHE_ENC_OCC)))
+// code-shape switches of the vector-op kernels (A/B and fault bisection):
+// wave-uniform loop trip counts in SGPRs, and per-lane operand choice by loading both
+// operands and selecting (never a per-lane buffer descriptor)
+#ifndef FPHE_UNIFORM_LOOPS
+#define FPHE_UNIFORM_LOOPS 1
+#endif
+#ifndef FPHE_SELECT_LOADS
+#define FPHE_SELECT_LOADS 1
+#endif
 #ifndef FPHE_POW_OCC
 #define FPHE_POW_OCC 3
 #endif
@@ -375,14 +391,21 @@ __global__ __launch_bounds__(kBlock) FPHE_OCC2 void k_encrypt_crt27(KeyArgs K, c
 }
 
 // ======================================================================================
-// ct-add (fixedpoint_paillier/src/lib.rs:301-333), 27-bit engine
+// ct-add (fixedpoint_paillier/src/lib.rs:301-333), 27-bit engine.
+// Slot i of the launch computes element ord[i] (ord == nullptr: element i), so the host can
+// hand the elements over in exponent-gap order -- a wave pays for its largest gap -- with
+// no gather or scatter copies: operands and results are addressed through whole-vector
+// buffer descriptors with a per-lane byte offset (the vector must be < 4 GiB, the host
+// splits larger ones).  Lanes past `count` get the descriptor's size as offset: their
+// loads return 0 and their stores are dropped by the hardware range check.
 // ======================================================================================
 template <int L>
 __global__ __launch_bounds__(kBlock) FPHE_OCC_MISC void k_add27(KeyArgs K, const u32* __restrict__ Ca, const u8* __restrict__ sa,
                                                   const int32_t* __restrict__ ea, const u32* __restrict__ Cb,
                                                   const u8* __restrict__ sb, const int32_t* __restrict__ eb,
-                                                  int bstride, size_t count, u32* __restrict__ Co,
-                                                  u8* __restrict__ so, int32_t* __restrict__ eo, u32 ldsw) {
+                                                  int bstride, size_t count, const int32_t* __restrict__ ord,
+                                                  u32* __restrict__ Co, u8* __restrict__ so, int32_t* __restrict__ eo,
+                                                  u32 ldsw) {
   constexpr int TPI = L / 32;
   using G = Geo<TPI>;
   constexpr int E = G::E;
@@ -396,23 +419,41 @@ __global__ __launch_bounds__(kBlock) FPHE_OCC_MISC void k_add27(KeyArgs K, const
   Mod<TPI> N;
   N.init(K.N2_27, g.q);
   const u32 np = K.n2_np27;
+  const u32 vbytes = (u32)((count + FPHE_WAVE - 1) / FPHE_WAVE) * L32 * 256u;
+  const __amdgpu_buffer_rsrc_t ra = rsrc(Ca, vbytes), ro = rsrc(Co, vbytes);
+  const __amdgpu_buffer_rsrc_t rb = rsrc(Cb, bstride ? vbytes : L32 * 256u);
+  // byte offset of word 32q of element e (tile-major [tiles][L][64])
+  auto voff = [&](size_t e) -> u32 { return (u32)(((e >> 6) * L32 + 32u * (u32)g.q) * FPHE_WAVE + (e & 63)) * 4u; };
+  auto io = [&](const __amdgpu_buffer_rsrc_t& r, u32 vb) {
+    asm volatile("" : "+v"(vb));  // opaque: word k stays "vb + k * 256" (instruction offset)
+    ColIO c;
+    c.r = r;
+    c.vb = vb;
+    return c;
+  };
+  // a lane's 1026-bit chunk spans words [32q, 32q + 34); the element's top lane must read
+  // 0 past word L-1 (the descriptor spans the whole vector, so the range check no longer
+  // does that: the next words belong to the next tile)
+  const bool top = g.q == TPI - 1;
+  auto ld = [&](const ColIO& c, int k) -> u32 {
+    const u32 v = c.ld(k);
+    return (k >= 32 && top) ? 0u : v;
+  };
   const u32 nwt = (u32)((count + E - 1) / E);
   for (u32 wt = gw; wt < nwt; wt += nw) {
-    const size_t ebase = (size_t)wt * E;
-    const u32 tile = (u32)(ebase >> 6);
-    const u32 col = (u32)(ebase & 63) + (u32)g.e;
-    const size_t elem = ebase + g.e;
+    const size_t slot = (size_t)wt * E + g.e;
+    const bool live = slot < count;
+    const size_t elem = !live ? 0 : (ord ? (size_t)(u32)ord[slot] : slot);
     const size_t be = bstride ? elem : 0;
-    const u32 bcolm = bstride ? col : 0u;
-    const ColIO Ai = colio(Ca + (size_t)tile * L32 * FPHE_WAVE, L32, col, 32u * g.q);
-    const ColIO Bi = colio(bstride ? Cb + (size_t)tile * L32 * FPHE_WAVE : Cb, L32, bcolm, 32u * g.q);
-    const ColIO Oo = colio(Co + (size_t)tile * L32 * FPHE_WAVE, L32, col, 32u * g.q);
+    const u32 vo = live ? voff(elem) : vbytes;
+    const ColIO Ai = io(ra, vo), Oo = io(ro, vo);
+    const ColIO Bi = io(rb, live ? voff(be) : (bstride ? vbytes : L32 * 256u));
     const int xa = ea[elem], xb = eb[be];
     const u32 sav = sa[elem], sbv = sb[be];
     const bool x_is_a = xa > xb;
     L27 A, Bv;
-    load_chunk(A, 2u * g.q, [&](int k) { return Ai.ld(k); });
-    load_chunk(Bv, 2u * g.q, [&](int k) { return Bi.ld(k); });
+    load_chunk(A, 2u * g.q, [&](int k) { return ld(Ai, k); });
+    load_chunk(Bv, 2u * g.q, [&](int k) { return ld(Bi, k); });
     // literal-1 tests (:303-308) over the element's lanes
     u32 za = 0, zb = 0;
 #pragma unroll
@@ -425,38 +466,49 @@ __global__ __launch_bounds__(kBlock) FPHE_OCC_MISC void k_add27(KeyArgs K, const
     zb = elem_or<TPI>(zb);
     const bool lit_a = za == 0 && sav == 0;
     const bool lit_b = zb == 0 && sbv == 0;
+    const bool lit = lit_a || lit_b;
     int d = x_is_a ? xa - xb : xb - xa;
-    if (lit_a || lit_b) d = 0;
+    if (lit || !live) d = 0;
     // x = higher-exp operand (stays in A); y is re-read at the end rather than held in
     // registers across the squarings
 #pragma unroll
     for (int j = 0; j < LL; ++j) A.set(j, x_is_a ? A[j] : Bv[j]);
     const_to_slot<TPI>(bcol, qoff, K.N2R2_27, g.q);
     mont_mul<TPI>(A, bcol, N, np, g.q);  // x R
-    const int nsq = wave_max_int(4 * d);
+    // the squaring count is wave-uniform (an SGPR): the loop's control flow is scalar and
+    // only the per-element `k < 4d` test masks lanes
+    const int nsq = __builtin_amdgcn_readfirstlane(wave_max_int(4 * d));
 #pragma unroll 1
     for (int k = 0; k < nsq; ++k) {
       if (k < 4 * d) sqr<TPI>(A, bcol, qoff, N, np, g.q);
     }
-    load_chunk(Bv, 2u * g.q, [&](int k) { return x_is_a ? Bi.ld(k) : Ai.ld(k); });
+    // y: both operands' words are read and selected per lane -- wave-uniform descriptors
+    // only (a per-lane descriptor becomes a readfirstlane loop around every load, which
+    // the register allocator broke at 3 waves/SIMD: DESIGN.md §3)
+    load_chunk(Bv, 2u * g.q, [&](int k) {
+      const u32 wa = ld(Ai, k), wb = ld(Bi, k);
+      return x_is_a ? wb : wa;
+    });
     to_slot<TPI>(bcol, qoff, Bv);
     mont_mul<TPI>(A, bcol, N, np, g.q);  // x^(16^d) y mod n^2 (< 2N)
     finalize<TPI>(A, N, g.q);
     const u32 sy = x_is_a ? sbv : sav;
     u32 sign = d == 0 ? (sav ^ sbv) : sy;
     int exo = xa < xb ? xa : xb;
-    if (lit_a || lit_b) {
+    if (lit) {
       // copy the other operand through untouched (words, not limbs: no re-encoding)
       sign = lit_a ? sbv : sav;
       exo = lit_a ? xb : xa;
     }
-    if (lit_a || lit_b) {
-#pragma unroll
-      for (int k = 0; k < 32; ++k) Oo.st(k, lit_a ? Bi.ld(k) : Ai.ld(k));
+    if (__builtin_amdgcn_readfirstlane((u32)__any(lit))) {  // wave-uniform branch
+      store_chunk<TPI>(A, g.q, [&](int k, u32 v) {
+        const u32 wa = Ai.ld(k), wb = Bi.ld(k);
+        Oo.st(k, lit ? (lit_a ? wb : wa) : v);
+      });
     } else {
       store_chunk<TPI>(A, g.q, [&](int k, u32 v) { Oo.st(k, v); });
     }
-    if (g.q == 0 && elem < count) {
+    if (g.q == 0 && live) {
       so[elem] = (u8)sign;
       eo[elem] = exo;
     }
@@ -573,9 +625,20 @@ __global__ __launch_bounds__(kBlock) FPHE_OCC_MISC void k_mul27(KeyArgs K, const
     const ColIO Ii = colio(Cinv + (size_t)tile * L32 * FPHE_WAVE, L32, col, 32u * g.q);
     const ColIO Oo = colio(Co + (size_t)tile * L32 * FPHE_WAVE, L32, col, 32u * g.q);
     const int ebits = inside ? ebits_in[elem] : 0;
+#if FPHE_UNIFORM_LOOPS
+    const int maxbits = __builtin_amdgcn_readfirstlane(wave_max_int(ebits));  // SGPR: scalar loop control
+#else
     const int maxbits = wave_max_int(ebits);
+#endif
     L27 A;
+#if FPHE_SELECT_LOADS
+    load_chunk(A, 2u * g.q, [&](int k) {  // both loads, per-lane select: wave-uniform descriptors
+      const u32 wi = Ii.ld(k), wa = Ai.ld(k);
+      return nd ? wi : wa;
+    });
+#else
     load_chunk(A, 2u * g.q, [&](int k) { return nd ? Ii.ld(k) : Ai.ld(k); });
+#endif
     const_to_slot<TPI>(bcol, qoff, K.N2R2_27, g.q);
     mont_mul<TPI>(A, bcol, N, np, g.q);  // X = base R
     if (maxbits > 0) {
@@ -645,7 +708,7 @@ __global__ __launch_bounds__(kBlock) FPHE_OCC_MISC void k_mul27(KeyArgs K, const
 constexpr int kFoldMax = 64;
 
 template <int L>
-__global__ __launch_bounds__(kBlock) FPHE_OCC_MISC void k_fold27(KeyArgs K, const u32* __restrict__ Src,
+__global__ __launch_bounds__(kBlock) FPHE_OCC_FOLD void k_fold27(KeyArgs K, const u32* __restrict__ Src,
                                                              const u8* __restrict__ ssign,
                                                              const int32_t* __restrict__ sexp,
                                                              const int64_t* __restrict__ ord,
@@ -690,7 +753,11 @@ __global__ __launch_bounds__(kBlock) FPHE_OCC_MISC void k_fold27(KeyArgs K, cons
     const bool inside = ch < nchunks;
     const int64_t st = inside ? cstart[ch] : 0;
     const int len = inside ? clen[ch] : 0;
+#if FPHE_UNIFORM_LOOPS
+    const int maxlen = __builtin_amdgcn_readfirstlane(wave_max_int(len));
+#else
     const int maxlen = wave_max_int(len);
+#endif
     L27 A, B;
     u32 W[34];
     u32 sg = 0;

@@ -31,10 +31,14 @@ def shard_bounds(count: int, rank: int, world: int) -> Tuple[int, int]:
     return min(t0 * WAVE, count), min(t1 * WAVE, count)
 
 
-def gather_tiles(C: torch.Tensor, sign: torch.Tensor, exp: torch.Tensor, count: int, group=None):
+def gather_tiles(C: torch.Tensor, sign: torch.Tensor, exp: torch.Tensor, count: int, group=None,
+                 trim: bool = True):
     """All-gather the per-rank shards (tile-major C [nt, L, 64], sign/exp [nt*64]) into the
     full vector on every rank.  Shards are padded to the largest shard for the collective
-    and trimmed after.  Returns (C, sign, exp, total_count)."""
+    and, with ``trim``, the padding tiles are cut out after (one copy of the gathered
+    vector).  Returns (C, sign, exp, total_count); with ``trim=False`` the padded buffers
+    as gathered ([world * nt_max] tiles, rank r's shard at tiles [r * nt_max, ...)) and the
+    per-rank counts instead of the total."""
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
@@ -68,6 +72,11 @@ def gather_tiles(C: torch.Tensor, sign: torch.Tensor, exp: torch.Tensor, count: 
     dist.all_gather_into_tensor(sg, pad_flat(sign.to(torch.int32)), group=group)
     eg = torch.empty(world * nt_max * WAVE, dtype=exp.dtype, device=dev)
     dist.all_gather_into_tensor(eg, pad_flat(exp), group=group)
+    if not trim:
+        return Cg, sg, eg, counts
+    if all(c == nt_max * WAVE for c in counts[:-1]) and (counts[-1] + WAVE - 1) // WAVE == nt_max:
+        # no padding tiles (only the last shard's partial tile, which is the vector's end)
+        return Cg, sg.to(torch.uint8), eg, sum(counts)
     # shards are whole tiles except possibly the last rank's: drop the per-rank padding
     Cs, ss, es = [], [], []
     for r, c in enumerate(counts):

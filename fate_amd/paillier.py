@@ -748,19 +748,21 @@ class Ciphertext:
 # --------------------------------------------------------------------------------------
 # kernel launchers
 # --------------------------------------------------------------------------------------
-ADD_SORT_MIN = 4096  # elements; below this the reorder costs more than it saves
+ADD_SORT_MIN = 4096  # elements; below this the sort costs more than it saves
+ADD_CHUNK = 1 << 22  # elements per fphe_add_ordered call (its C vector must stay < 4 GiB)
 
 
 def _add_order(ea: torch.Tensor, eb: torch.Tensor, L2: int) -> Optional[torch.Tensor]:
-    """Element order for fphe_add that groups equal exponent gaps.
+    """Launch order for fphe_add_ordered that groups equal exponent gaps.
 
     Aligning the higher-exponent operand costs 4*|ea - eb| Montgomery squarings
     (decrese_exp_to, fixedpoint_paillier/src/lib.rs:250-258), and k_add27 runs every element
     of a wave for the wave's largest gap (the lanes of a wave share one instruction stream).
     With float data the gaps differ from element to element, so most waves pay for an
-    outlier; sorted by gap, a wave's elements need the same number of squarings.  Returns
-    the (stable) permutation, or None when it would save less than a quarter of the
-    modular products (the two gathers and the scatter around the kernel cost ~2 ms per 1M)."""
+    outlier; sorted by gap, a wave's elements need the same number of squarings.  The kernel
+    reads and writes the elements in place through the order (no gather or scatter
+    copies), so the only cost is the sort.  Returns the (stable) int32 permutation, or None
+    when it would save less than 5% of the modular products."""
     d = (ea.to(torch.int32) - eb.to(torch.int32)).abs()
     per_wave = WAVE // (L2 // 32)  # elements per wave: TPI = L2/32 lanes per element
     pad = (-d.numel()) % per_wave
@@ -772,9 +774,9 @@ def _add_order(ea: torch.Tensor, eb: torch.Tensor, L2: int) -> Optional[torch.Te
 
     ds, order = torch.sort(d, stable=True)
     c = torch.stack([cost(d), cost(ds)]).tolist()
-    if c[1] > 0.75 * c[0]:
+    if c[1] > 0.95 * c[0]:
         return None
-    return order
+    return order.to(torch.int32)
 
 
 def _add(pk: "PK", a: CiphertextVector, b: CiphertextVector, broadcast: bool, count: Optional[int] = None,
@@ -787,18 +789,22 @@ def _add(pk: "PK", a: CiphertextVector, b: CiphertextVector, broadcast: bool, co
     out = CiphertextVector.empty(n, a.L2, dev)
     if n == 0:
         return out
-    if reorder and not broadcast and n >= ADD_SORT_MIN:
-        order = _add_order(a.exp[:n], b.exp[:n], a.L2)
-        if order is not None:
-            # the same element-wise results, computed in exponent-gap order
-            o = _add(pk, a._gather(order), b._gather(order), False, n, reorder=False)
-            out._assign(order, o)
-            return out
     lib = _lib.load()
     ctx = pk._key.ctx(dev)
-    _lib.check(lib.fphe_add(ctx, _ptr(a.C), _ptr(a.sign), _ptr(a.exp), _ptr(b.C), _ptr(b.sign), _ptr(b.exp),
-                            0 if broadcast else 1, n, _ptr(out.C), _ptr(out.sign), _ptr(out.exp),
-                            ctypes.c_void_p(_stream(dev))), "fphe_add")
+    stream = ctypes.c_void_p(_stream(dev))
+    for s0 in range(0, n, ADD_CHUNK):  # whole tiles per chunk
+        m = min(ADD_CHUNK, n - s0)
+        t0, t1 = s0 // WAVE, _ntiles(s0 + m)
+        e0, e1 = s0, t1 * WAVE
+        order = None
+        if reorder and not broadcast and m >= ADD_SORT_MIN:
+            order = _add_order(a.exp[s0:s0 + m], b.exp[s0:s0 + m], a.L2)
+        bC, bs, be = (b.C, b.sign, b.exp) if broadcast else (b.C[t0:t1], b.sign[e0:e1], b.exp[e0:e1])
+        _lib.check(lib.fphe_add_ordered(ctx, _ptr(a.C[t0:t1]), _ptr(a.sign[e0:e1]), _ptr(a.exp[e0:e1]), _ptr(bC),
+                                        _ptr(bs), _ptr(be), 0 if broadcast else 1, m, _ptr(order),
+                                        _ptr(out.C[t0:t1]), _ptr(out.sign[e0:e1]), _ptr(out.exp[e0:e1]), stream),
+                   "fphe_add_ordered")
+        del order  # the launch is stream-ordered: the allocator reuses the block only after it
     return out
 
 

@@ -149,6 +149,19 @@ fphe_status fphe_add(fphe_ctx* ctx,
                      const uint32_t* Cb, const uint8_t* sb, const int32_t* eb, int b_stride,
                      size_t count, uint32_t* Co, uint8_t* so, int32_t* eo, void* stream);
 
+/* fphe_add computing element order[i] in launch slot i (order: DEVICE int32 [count], a
+ * permutation of [0, count); NULL = identity).  Same results, element for element, as
+ * fphe_add: the order only groups elements whose exponent gaps (4 squarings per step of
+ * decrese_exp_to, fixedpoint_paillier/src/lib.rs:250-258) are equal, so that each wave
+ * runs the squarings its own elements need.  With an order, count * L2 * 4 bytes must
+ * stay below 4 GiB - 1 MiB (FPHE_ERR_ARG otherwise; fphe_add itself splits larger
+ * vectors). */
+fphe_status fphe_add_ordered(fphe_ctx* ctx,
+                             const uint32_t* Ca, const uint8_t* sa, const int32_t* ea,
+                             const uint32_t* Cb, const uint8_t* sb, const int32_t* eb, int b_stride,
+                             size_t count, const int32_t* order, uint32_t* Co, uint8_t* so, int32_t* eo,
+                             void* stream);
+
 /* Ciphertext x plaintext: CiphertextVector.mul (paillier.rs:361) -> Ciphertext::mul
  * (fixedpoint_paillier/src/lib.rs:334-349).  Plaintext (P[T][lp][64], neg, pexp);
  * p_stride = 0 broadcasts element 0 (mul_scalar, paillier.rs:364). */
@@ -230,6 +243,16 @@ fphe_status fphe_wire_scan(const uint8_t* buf, size_t nbytes, size_t pos, size_t
                            int32_t* dig_len, uint8_t* neg, int32_t* exp, int32_t* radix, size_t* end);
 fphe_status fphe_wire_decode(const uint8_t* buf, const int64_t* dig_off, const int32_t* dig_len, uint32_t L,
                              size_t count, uint32_t* mag, int32_t* err, void* stream);
+
+/* Known-answer hook for the device CSPRNG behind the obfuscation nonces (fphe_encrypt with
+ * r == NULL draws r from ChaCha20, chacha_dev.h; the reference's r comes from
+ * StdRng::from_entropy(), math/src/rug/random.rs:15-25, so only the generator's correctness
+ * can be pinned, not its outputs).  out[i*16 .. i*16+16) = the RFC 8439 block function of
+ * (key, counter + i, nonce) for i < nblocks; out is a DEVICE buffer of 16*nblocks words.
+ * The encryption kernels select element e's stream as counter = block | (e >> 32) << 16,
+ * nonce = {e mod 2^32, call nonce hi, call nonce lo}. */
+fphe_status fphe_chacha20_blocks(const uint32_t key[8], uint32_t counter, const uint32_t nonce[3], size_t nblocks,
+                                 uint32_t* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -193,7 +193,7 @@ typedef struct {
   gref_ctx* c;
   long count;
   unsigned long seed;
-  int op;  /* 0 encrypt(obfuscated), 1 decrypt, 2 add */
+  int op;  /* 0 encrypt(obfuscated), 1 decrypt, 2 add (aligned), 3 add (Hetero-LR exponent gaps) */
   double secs;
 } job_t;
 
@@ -237,8 +237,24 @@ static void* run_job(void* arg) {
       __gmpz_mul(nude, nude, c->p);
       __gmpz_add(nude, nude, dp);
       if (SGN(nude) < 0) __gmpz_add(nude, nude, c->n);
-    } else {
+    } else if (j->op == 2) {
       __gmpz_mul(t, acc, o);
+      __gmpz_tdiv_r(acc, t, c->ns);
+    } else {
+      /* Ciphertext::add with exponent alignment (fixedpoint_paillier/src/lib.rs:301-333):
+         decrese_exp_to (:250-258) raises the higher-exp operand to 16^gap through mul_pt
+         (mpz_powm), then add_ct (paillier/src/lib.rs:35-37).  Gaps drawn as measured on the
+         bench's Hetero-LR-shaped adds (profiles/r01f_add_leg.txt): 0 for 37%, 1 for 58%,
+         2 for 5% of the elements. */
+      const unsigned g = (unsigned)(i % 100);
+      const unsigned gap = g < 37 ? 0u : (g < 95 ? 1u : 2u);
+      if (gap) {
+        __gmpz_set_ui(m, 1ul << (4 * gap));
+        __gmpz_powm(r, o, m, c->ns);
+        __gmpz_mul(t, acc, r);
+      } else {
+        __gmpz_mul(t, acc, o);
+      }
       __gmpz_tdiv_r(acc, t, c->ns);
     }
   }

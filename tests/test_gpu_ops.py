@@ -34,9 +34,16 @@ def env(request):
     return load(request.param)
 
 
-@pytest.fixture(scope="module")
-def env1024():
-    return load(1024)
+def more(opk, cts, k, seed=0):
+    """cts extended to k ciphertexts with random signed integers in (-n^2, n^2) and small
+    exponents: the vector algebra is exact integer arithmetic on any such values (they need
+    not be encryptions), and the oracle at 2048 bits costs ~0.14 s per real encryption."""
+    rng = random.Random(1000 + seed)
+    out = list(cts)
+    while len(out) < k:
+        c = rng.randrange(2, opk.ns)
+        out.append(O.Ciphertext(-c if rng.random() < 0.3 else c, rng.choice([0, -13, -14, -12])))
+    return out
 
 
 def dev_vec(pk, cts):
@@ -149,11 +156,11 @@ def test_mul_invert_branches_batch(env, count):
     assert host(pk, got) == ref([want[i] for i in pick])
 
 
-def test_mul_plaintext_edges(env1024):
+def test_mul_plaintext_edges(env):
     """Edges of Ciphertext::mul's classification (lib.rs:334-349).  For odd n,
     max_int + 1 == n - max_int, so no significand below n is "invalid"; P > n takes the
     inverse branch with a negative exponent, which GMP turns back into c^(P - n)."""
-    fx, sk, pk, coder, opk, cts = env1024
+    fx, sk, pk, coder, opk, cts = env
     sigs = [opk.max_int, opk.max_int + 1, opk.n - 1, opk.n, opk.n + 5, 0]
     c = cts[:len(sigs)]
     pv = P.PlaintextVector.from_ints(sigs, [0] * len(sigs))
@@ -161,19 +168,20 @@ def test_mul_plaintext_edges(env1024):
     assert host(pk, dev_vec(pk, c).mul(pk, pv)) == ref(want)
 
 
-def test_pack_squeeze(env1024):
-    fx, sk, pk, coder, opk, cts = env1024
+def test_pack_squeeze(env):
+    fx, sk, pk, coder, opk, cts = env
     data = cts[:23]  # ragged last chunk
     for pack_num, shift in ((2, 77), (3, 20), (1, 5)):
         got = dev_vec(pk, data).pack_squeeze(pack_num, shift, pk)
         assert host(pk, got) == ref(O.pack_squeeze(opk, data, pack_num, shift))
 
 
-def test_iupdate_and_masks(env1024):
-    fx, sk, pk, coder, opk, cts = env1024
+def test_iupdate_and_masks(env):
+    fx, sk, pk, coder, opk, cts = env
     rng = random.Random(7)
     stride = 2
     data = [O.ct_zero() for _ in range(10 * stride)]
+    cts = more(opk, cts, 91)
     data[3] = cts[90]  # a non-zero slot that also receives contributions
     other = cts[:20 * stride]
     indexes = [[rng.randrange(10) for _ in range(rng.randrange(0, 4))] for _ in range(20)]
@@ -193,24 +201,24 @@ def test_iupdate_and_masks(env1024):
 
 def _fold_terms(opk, count, seed):
     """Terms for the segmented fold: long equal-exponent runs (> 64, several fphe_fold
-    rounds), negative significands (sign 1), other exponents, literal 1s with exponent 0
-    and -14 (the nude encryption of 0.0 is the integer 1, which add() treats as zero)."""
+    rounds), negative ciphertext integers (sign 1), other exponents, literal 1s with
+    exponent 0 and -14 (the nude encryption of 0.0 is the integer 1, which add() treats as
+    zero)."""
     rng = random.Random(seed)
     terms = []
     for i in range(count):
         exp = rng.choice([0, 0, 0, 0, -3, 2, -1])
-        sig = rng.randrange(1, 1 << 40) * rng.choice([1, -1])
-        pt = O.Plaintext(sig if sig >= 0 else sig, exp)
-        terms.append(O.fp_encrypt(opk, pt, True, 1 + rng.randrange(opk.n - 1)))
+        c = rng.randrange(2, opk.ns)  # any integer works for the fold's algebra (see more())
+        terms.append(O.Ciphertext(-c if rng.random() < 0.5 else c, exp))  # signed, as encryptions of negatives
     terms[5] = O.fp_encrypt(opk, O.encode_f64(opk.n, 0.0), False)  # integer 1, exp -14
     terms[9] = O.ct_zero()
     return terms
 
 
-def test_iupdate_long_segments(env1024):
+def test_iupdate_long_segments(env):
     """iupdate with hundreds of terms per slot: exercises fphe_fold's multi-round chunking
     and the per-exponent merge against the reference's sequential fold."""
-    fx, sk, pk, coder, opk, cts = env1024
+    fx, sk, pk, coder, opk, cts = env
     rng = random.Random(11)
     stride = 1
     other = _fold_terms(opk, 420, 3)
@@ -226,8 +234,8 @@ def test_iupdate_long_segments(env1024):
     assert host(pk, v) == ref(want)
 
 
-def test_chunking_cumsum_with_step(env1024):
-    fx, sk, pk, coder, opk, cts = env1024
+def test_chunking_cumsum_with_step(env):
+    fx, sk, pk, coder, opk, cts = env
     data = cts[:24]
     for sizes, step in (([4, 2, 6], 2), ([12, 12], 1), ([24], 3)):
         v = dev_vec(pk, data)
@@ -237,16 +245,16 @@ def test_chunking_cumsum_with_step(env1024):
         assert host(pk, v) == ref(want)
 
 
-def test_intervals_sum_with_step(env1024):
-    fx, sk, pk, coder, opk, cts = env1024
+def test_intervals_sum_with_step(env):
+    fx, sk, pk, coder, opk, cts = env
     data = cts[:30]
     intervals, step = [(0, 7), (7, 7), (10, 30)], 3
     got = dev_vec(pk, data).intervals_sum_with_step(pk, intervals, step)
     assert host(pk, got) == ref(O.intervals_sum_with_step(opk, data, intervals, step))
 
 
-def test_matmul_rmatmul(env1024):
-    fx, sk, pk, coder, opk, cts = env1024
+def test_matmul_rmatmul(env):
+    fx, sk, pk, coder, opk, cts = env
     rng = random.Random(3)
     # a: 3x4 ciphertexts; b: 4x2 plaintexts with negative entries (invert branch)
     a = cts[:12]
@@ -273,8 +281,8 @@ def _self_op_ref(opk, data, sa, sb, size, sub):
     return data
 
 
-def test_iadd_isub_vec_self(env1024):
-    fx, sk, pk, coder, opk, cts = env1024
+def test_iadd_isub_vec_self(env):
+    fx, sk, pk, coder, opk, cts = env
     data = cts[:20]
     for sa, sb, size in ((0, 3, 10), (5, 1, None), (4, 4, 6), (0, 10, 10)):
         for sub in (False, True):
@@ -319,10 +327,10 @@ def test_int_codec(env):
     assert coder.decode_i32_vec(pv_ok) == want32
 
 
-def test_pack_unpack_floats(env1024):
+def test_pack_unpack_floats(env):
     """pack_floats / unpack_floats on the device vs the oracle (lib.rs:79-118), SecureBoost
     shape: g+1 and h packed at precision 52 with offset 77 (guest.py:203-206)."""
-    fx, sk, pk, coder, opk, cts = env1024
+    fx, sk, pk, coder, opk, cts = env
     rng = random.Random(4)
     vals = []
     for _ in range(37):

@@ -3,6 +3,7 @@ golden fixtures produced by the oracle (tests/golden/make_fixtures.py), bit-exac
 
 Integer work => bit-exact equality of signed ciphertext integers, exponents and decoded
 float bits (no tolerance)."""
+import ctypes
 import json
 import os
 import struct
@@ -119,3 +120,69 @@ def test_roundtrip_device_rng(fx, keyholder):
     # two encryptions of the same plaintext differ (fresh r per element and per call)
     ct2 = pk.encrypt_encoded(coder.encode_f32_vec(x), True)
     assert not torch.equal(ct.C, ct2.C)
+
+
+F64_EDGES = [
+    0.0, -0.0, 1.0, -1.0, 0.5, 1.5, -2.5, 0.1, 1.0 / 3.0, -7.0 / 3.0,
+    5e-324, -5e-324, 1e-323, 3 * 2.0 ** -1074, 2.2250738585072009e-308, -2.2250738585072009e-308,  # subnormals
+    2.2250738585072014e-308, -2.2250738585072014e-308, 2.0 ** -1022 * 1.5,                          # smallest normals
+    1.7976931348623157e308, -1.7976931348623157e308, 2.0 ** 1023, 8.98846567431158e307,             # largest
+    2.0 ** 52, 2.0 ** 52 + 1, 2.0 ** 53, 2.0 ** 53 - 1, 2.0 ** 53 + 2, -(2.0 ** 63), 2.0 ** 64 - 2048,
+    float.fromhex("0x1.fffffffffffffp-1"), float.fromhex("0x1.0000000000001p+0"),                    # ulp around 1
+    float.fromhex("0x1.8p-1070"), float.fromhex("-0x1.000001p+100"), 3.4028234663852886e38, 1e-30,
+]
+
+
+def test_encode_f64_bit_exact(fx):
+    """Device k_encode_f64 against the oracle's Coder::encode_f64 (fixedpoint_paillier/src/
+    lib.rs:148-168: frexp, exp = floor((e - 53) / 4), significand = round_half_away(x 16^-exp),
+    zero -> (0, -14)) on subnormals down to 4.9e-324, the largest normals, ulp neighbours and
+    a seeded random sweep over the whole exponent range."""
+    from oracle import paillier_oracle as O
+    f, sk, pk, coder = fx
+    n = int(f["p"], 16) * int(f["q"], 16)
+    rng = np.random.default_rng(17)
+    bits = rng.integers(0, 2 ** 63, 2000, dtype=np.uint64) | (rng.integers(0, 2, 2000, dtype=np.uint64) << np.uint64(63))
+    rand = [float(v) for v in bits.view(np.float64) if np.isfinite(v)]
+    xs = F64_EDGES + rand
+    pv = coder.encode_f64_vec(torch.tensor(xs, dtype=torch.float64).cuda())
+    sig, exp = pv.to_ints()
+    want = [O.encode_f64(n, x) for x in xs]
+    assert exp == [w.exp for w in want]
+    assert sig == [w.significant for w in want]
+
+
+@pytest.mark.parametrize("bad", [float("inf"), float("-inf"), float("nan")])
+def test_encode_f64_nonfinite_panics(fx, bad):
+    """Non-finite floats: the reference's to_integer().unwrap() panics (lib.rs:152-157)."""
+    f, sk, pk, coder = fx
+    with pytest.raises(P.PanicException):
+        coder.encode_f64_vec(torch.tensor([1.0, bad, 2.0], dtype=torch.float64).cuda())
+
+
+def test_chacha20_rfc8439_block():
+    """Device ChaCha20 block function (the CSPRNG of the obfuscation nonces, chacha_dev.h)
+    against RFC 8439 §2.3.2's test vector and the same restatement the CPU suite pins
+    (tests/test_host.py), over many counters and nonces."""
+    from fate_amd import _lib
+    from tests.chacha_ref import RFC8439_232, chacha20_block
+    lib = _lib.load()
+    key, counter, nonce, want = RFC8439_232
+    kk = (ctypes.c_uint32 * 8)(*key)
+    nn = (ctypes.c_uint32 * 3)(*nonce)
+    out = torch.zeros(16 * 300, dtype=torch.int32, device="cuda")
+    _lib.check(lib.fphe_chacha20_blocks(kk, counter, nn, 300, ctypes.c_void_p(out.data_ptr()), None),
+               "fphe_chacha20_blocks")
+    torch.cuda.synchronize()
+    got = [v & 0xffffffff for v in out.cpu().tolist()]
+    assert got[:16] == want
+    for i in (1, 2, 77, 299):
+        assert got[16 * i:16 * i + 16] == chacha20_block(key, counter + i, nonce)
+    # the stream selector of draw_r for an element index above 2^32 (bits 32..47 in the counter)
+    e = (3 << 32) + 12345
+    nn2 = (ctypes.c_uint32 * 3)(e & 0xffffffff, 0xdeadbeef, 0x01234567)
+    _lib.check(lib.fphe_chacha20_blocks(kk, (e >> 32) << 16, nn2, 2, ctypes.c_void_p(out.data_ptr()), None),
+               "fphe_chacha20_blocks")
+    torch.cuda.synchronize()
+    got = [v & 0xffffffff for v in out[:32].cpu().tolist()]
+    assert got[:16] == chacha20_block(key, 3 << 16, [e & 0xffffffff, 0xdeadbeef, 0x01234567])

@@ -5,20 +5,44 @@ There the PHETensor layer (tensor/phe/_ops.py:52-266) turns torch.add(enc, enc) 
 evaluator.add, torch.add(enc, 1) into add_plain_scalar, torch.add(enc, t) into add_plain,
 and so on.  The reference tests only print; here the decrypted results are checked against
 the float computation.  Inputs are CPU tensors, as in the reference."""
+import json
+import os
+
 import pytest
 import torch
 
+from fate_amd import paillier as P
 from fate_amd import protocol as PR
+from oracle import paillier_oracle as O
 
 pytestmark = pytest.mark.gpu
 
+HERE = os.path.dirname(os.path.abspath(__file__))
 EV = PR.evaluator
 X = torch.tensor([[1.0, 2.0, 3.0, 4.0], [5.0, 6.0, 7.0, -8.0]])
 
 
-@pytest.fixture(scope="module")
-def keys():
-    return PR.keygen(1024)
+def fixture_keys(bits):
+    """The seam's (SK, PK, Coder) over the golden fixture's primes, plus the oracle's keys."""
+    with open(os.path.join(HERE, "golden", f"paillier_{bits}.json")) as f:
+        fx = json.load(f)
+    p, q = int(fx["p"], 16), int(fx["q"], 16)
+    sk, pk, coder = P.keypair_from_primes(p, q)
+    return (PR.SK(sk), PR.PK(pk), PR.Coder(coder)), O.keypair_from_primes(p, q)[1]
+
+
+@pytest.fixture(scope="module", params=["keygen1024", "fixture2048"])
+def keys(request):
+    # the reference's tests use keygen(1024) (test_vertor_paillier.py:12); 2048 is the
+    # BASELINE key size
+    if request.param == "keygen1024":
+        return PR.keygen(1024)
+    return fixture_keys(2048)[0]
+
+
+@pytest.fixture(scope="module", params=[1024, 2048])
+def okeys(request):
+    return fixture_keys(request.param)
 
 
 def enc(keys, x):
@@ -101,3 +125,61 @@ def test_slice_cat_update_cumsum(keys):
     assert torch.equal(dec(keys, h, torch.float64, (3,)), want)
     EV.chunking_cumsum_with_step(pk, e, [6, 6], 1)
     assert torch.equal(dec(keys, e, torch.float64, (12,)), torch.cat([v[:6].cumsum(0), v[6:].cumsum(0)]))
+
+
+# ---- bit-exact through the seam: every evaluator result against the oracle applied to the
+# same device inputs (the obfuscated encryptions' integers are read back first, so the random
+# r does not matter) ----------------------------------------------------------------------
+def signed(pk, v):
+    c, e = v.to_signed_ints(pk.pk.ns)
+    return [O.Ciphertext(a, b) for a, b in zip(c, e)]
+
+
+def pts(coder, t):
+    sig, exp = coder.encode_tensor(t).to_ints()
+    return [O.Plaintext(a, b) for a, b in zip(sig, exp)]
+
+
+def pair(o):
+    return [(c.c, c.exp) for c in o]
+
+
+def test_bitexact_add_sub_plain(okeys):
+    (sk, pk, coder), opk = okeys
+    g = torch.Generator().manual_seed(21)
+    a, b = torch.randn(37, generator=g), torch.randn(37, generator=g) * 1e-3
+    ea, eb = enc((sk, pk, coder), a), enc((sk, pk, coder), b)
+    A, B = signed(pk, ea), signed(pk, eb)
+    assert pair(signed(pk, EV.add(ea, eb, pk))) == pair(O.vec_add(opk, A, B))
+    assert pair(signed(pk, EV.sub(ea, eb, pk))) == pair(O.vec_sub(opk, A, B))
+    assert pair(signed(pk, EV.rsub(ea, eb, pk))) == pair(O.vec_rsub(opk, A, B))
+    # add_plain = encode + encrypt(obfuscate=False) + add (paillier.py:185-191)
+    y = torch.randn(37, generator=g).double()
+    want = [O.ct_add(opk, x, O.fp_encrypt(opk, p, False)) for x, p in zip(A, pts(coder, y))]
+    assert pair(signed(pk, EV.add_plain(ea, y, pk, coder))) == pair(want)
+
+
+def test_bitexact_mul_plain(okeys):
+    (sk, pk, coder), opk = okeys
+    g = torch.Generator().manual_seed(22)
+    a = torch.randn(33, generator=g)
+    w = torch.randn(33, generator=g).double() * 3  # negative weights: the invert branch
+    ea = enc((sk, pk, coder), a)
+    want = O.vec_mul(opk, signed(pk, ea), pts(coder, w))
+    assert pair(signed(pk, EV.mul_plain(ea, w, pk, coder))) == pair(want)
+    wi = torch.randint(-1000, 1000, (33,), generator=g, dtype=torch.int64)  # encoded negative ints
+    want = O.vec_mul(opk, signed(pk, ea), pts(coder, wi))
+    assert pair(signed(pk, EV.mul_plain(ea, wi, pk, coder))) == pair(want)
+
+
+def test_bitexact_matmul_rmatmul(okeys):
+    (sk, pk, coder), opk = okeys
+    g = torch.Generator().manual_seed(23)
+    x, y = torch.randn(5, 3, generator=g), torch.randn(3, 4, generator=g).double()
+    ex = enc((sk, pk, coder), x)
+    got = EV.matmul(ex, y, [5, 3], [3, 4], pk, coder, torch.float64)
+    assert pair(signed(pk, got)) == pair(O.matmul(opk, signed(pk, ex), pts(coder, y), [5, 3], [3, 4]))
+    # Hetero-LR host: X^T enc(d) with int64-encoded features (coordinated_lr/host.py:242)
+    xi = torch.randint(-50, 50, (4, 3), generator=g, dtype=torch.int64)
+    got = EV.rmatmul(ex, xi, [3, 5], [4, 3], pk, coder, torch.int64)
+    assert pair(signed(pk, got)) == pair(O.rmatmul(opk, signed(pk, ex), pts(coder, xi), [3, 5], [4, 3]))

@@ -105,3 +105,18 @@ def test_tile_gather_assign_cat_plumbing():
     rows = P.gather_rows(t, idx)
     assert torch.equal(rows, cols[:, idx].T)
     assert torch.equal(P.rows_to_tile_tensor(rows), P.cols_to_tiles(cols[:, idx]))
+
+
+def test_chacha20_reference_pinned_by_rfc8439():
+    """The Python ChaCha20 restatement the device CSPRNG is checked against reproduces RFC
+    8439 §2.3.2 (state words and serialized keystream)."""
+    from tests.chacha_ref import RFC8439_232, RFC8439_232_SERIALIZED, chacha20_block
+    key, counter, nonce, want = RFC8439_232
+    got = chacha20_block(key, counter, nonce)
+    assert got == want
+    assert b"".join(w.to_bytes(4, "little") for w in got) == RFC8439_232_SERIALIZED
+
+
+def test_chacha20_symbol_exported():
+    from fate_amd import _lib
+    assert "fphe_chacha20_blocks" in _lib.EXPORTED_SYMBOLS

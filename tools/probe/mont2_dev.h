@@ -15,7 +15,7 @@
 // the rate two waves reach (profiles/r01_probe_alu.txt).  Two lanes per element halve
 // the per-lane footprint (~210 VGPRs) so two waves share each SIMD.
 #pragma once
-#include "mont_dev.h"
+#include "../../fate_amd/csrc/mont_dev.h"
 
 namespace fphe {
 

@@ -4,7 +4,7 @@
 #include <cstdio>
 #include <cstdint>
 #include <vector>
-#include "../../fate_amd/csrc/mont2_dev.h"
+#include "mont2_dev.h"  // the round-1 32-bit two-lane engine, kept with the probe
 
 using namespace fphe;
 
