@@ -117,10 +117,10 @@ def load() -> ctypes.CDLL:
         sz = ctypes.c_size_t
         lib.fphe_chacha20_blocks.argtypes = [vp, ctypes.c_uint32, vp, sz, vp, vp]
         lib.fphe_chacha20_blocks.restype = st
-        lib.fphe_wire_lengths.argtypes = [vp, vp, ctypes.c_uint32, sz, vp, vp]
-        lib.fphe_wire_encode.argtypes = [vp, vp, vp, ctypes.c_uint32, sz, vp, vp, vp, vp]
+        lib.fphe_wire_lengths.argtypes = [vp, vp, ctypes.c_uint32, sz, vp, vp, vp]
+        lib.fphe_wire_encode.argtypes = [vp, vp, vp, ctypes.c_uint32, sz, vp, vp, vp, vp, vp]
         lib.fphe_wire_scan.argtypes = [vp, sz, sz, sz, vp, vp, vp, vp, vp, vp]
-        lib.fphe_wire_decode.argtypes = [vp, vp, vp, ctypes.c_uint32, sz, vp, vp, vp]
+        lib.fphe_wire_decode.argtypes = [vp, vp, vp, vp, ctypes.c_uint32, sz, vp, vp, vp]
         for name in ("fphe_wire_lengths", "fphe_wire_encode", "fphe_wire_scan", "fphe_wire_decode"):
             getattr(lib, name).restype = st
         _lib = lib

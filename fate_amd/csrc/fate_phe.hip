@@ -812,29 +812,48 @@ fphe_status launch_mul27(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, con
 //   i32 radix | u64 len | len ASCII chars ("-"? + digits, no leading zeros) | i32 exp
 // (BInt is a newtype over rug::Integer, math/src/rug/mod.rs:11; rug's serde writes an
 // Integer as the struct {radix, value}; pickles are bincode::serialize, paillier.rs:219-226).
-// Radix 16, lowercase.  mag is element-major LSF uint32 [count][L] (fphe_export_signed).
-__device__ __forceinline__ u32 wire_digits(const u32* __restrict__ m, u32 L) {
+// rug picks the radix per value: decimal when the magnitude has at most 32 significant bits,
+// lowercase hex otherwise (rug 1.20 integer/serde.rs; unpinned).  mag is
+// element-major LSF uint32 [count][L] (fphe_export_signed).
+__device__ __forceinline__ u32 dec_digits(u32 w) {
+  u32 d = 1;
+  for (u64 p = 10; p <= w; p *= 10) ++d;
+  return d;
+}
+
+// digits and radix of one magnitude
+__device__ __forceinline__ u32 wire_digits(const u32* __restrict__ m, u32 L, u32& radix) {
   int k = (int)L - 1;
   while (k > 0 && m[k] == 0) --k;
   const u32 w = m[k];
-  const u32 nib = w ? (32u - (u32)__builtin_clz(w) + 3u) / 4u : 1u;
+  if (k == 0) {
+    radix = 10;
+    return dec_digits(w);
+  }
+  radix = 16;
+  const u32 nib = (32u - (u32)__builtin_clz(w) + 3u) / 4u;
   return (u32)k * 8u + nib;
 }
 
 __global__ __launch_bounds__(256) void k_wire_lengths(const u32* __restrict__ mag, const u8* __restrict__ neg, u32 L,
-                                                      size_t count, int64_t* __restrict__ rec_len) {
+                                                      size_t count, int64_t* __restrict__ rec_len,
+                                                      u8* __restrict__ radix) {
   const size_t e = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= count) return;
-  rec_len[e] = 4 + 8 + 4 + (int64_t)(neg[e] ? 1 : 0) + (int64_t)wire_digits(mag + e * L, L);
+  u32 rdx;
+  const u32 nd = wire_digits(mag + e * L, L, rdx);
+  rec_len[e] = 4 + 8 + 4 + (int64_t)(neg[e] ? 1 : 0) + (int64_t)nd;
+  radix[e] = (u8)rdx;
 }
 
-// one thread per (element, 32-bit word): the word's 8 nibbles are digit positions
-// 8k .. 8k+7 from the least significant end; word 0's thread also writes the header,
-// the sign and the exponent.
+// one thread per (element, 32-bit word): for a hex record the word's 8 nibbles are digit
+// positions 8k .. 8k+7 from the least significant end; word 0's thread also writes the
+// header, the sign and the exponent, and all digits of a decimal (<= 32-bit) record.
 __global__ __launch_bounds__(256) void k_wire_encode(const u32* __restrict__ mag, const u8* __restrict__ neg,
                                                      const int32_t* __restrict__ exp, u32 L, size_t count,
                                                      const int64_t* __restrict__ rec_off,
-                                                     const int64_t* __restrict__ rec_len, u8* __restrict__ out) {
+                                                     const int64_t* __restrict__ rec_len, const u8* __restrict__ radix,
+                                                     u8* __restrict__ out) {
   const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= count * L) return;
   const size_t e = t / L;
@@ -842,19 +861,29 @@ __global__ __launch_bounds__(256) void k_wire_encode(const u32* __restrict__ mag
   const u32* m = mag + e * L;
   const u32 sg = neg[e] ? 1u : 0u;
   const u32 digits = (u32)(rec_len[e] - 16 - sg);
-  if (8u * k >= digits) return;
+  const u32 rdx = radix[e];
+  if (rdx == 10 && k != 0) return;
+  if (rdx != 10 && 8u * k >= digits) return;
   u8* r = out + rec_off[e];
+  u8* d = r + 12 + sg;
   if (k == 0) {
     const uint64_t len = digits + sg;
-    r[0] = 16; r[1] = 0; r[2] = 0; r[3] = 0;
+    r[0] = (u8)rdx; r[1] = 0; r[2] = 0; r[3] = 0;
     for (int b = 0; b < 8; ++b) r[4 + b] = (u8)(len >> (8 * b));
     if (sg) r[12] = '-';
     const u32 x = (u32)exp[e];
     u8* ex = r + 12 + sg + digits;
     for (int b = 0; b < 4; ++b) ex[b] = (u8)(x >> (8 * b));
+    if (rdx == 10) {
+      u32 w = m[0];
+      for (u32 j = 0; j < digits; ++j) {
+        d[digits - 1 - j] = (u8)('0' + w % 10u);
+        w /= 10u;
+      }
+      return;
+    }
   }
   const u32 w = m[k];
-  u8* d = r + 12 + sg;
   for (u32 i = 0; i < 8; ++i) {
     const u32 j = 8u * k + i;
     if (j >= digits) break;
@@ -863,18 +892,39 @@ __global__ __launch_bounds__(256) void k_wire_encode(const u32* __restrict__ mag
   }
 }
 
-// radix-16 digit strings back to magnitude words; err bit 0: a non-hex character,
-// bit 1: more significant digits than L words hold (after leading zeros).
+// digit strings back to magnitude words (radix 16: one thread per word; radix 10 with at
+// most 19 digits: word 0's thread writes words 0 and 1; other radixes are parsed on the
+// host).  err bit 0: a character that is not a digit of the radix, bit 1: a value wider
+// than L words.
 __global__ __launch_bounds__(256) void k_wire_decode(const u8* __restrict__ buf, const int64_t* __restrict__ dig_off,
-                                                     const int32_t* __restrict__ dig_len, u32 L, size_t count,
-                                                     u32* __restrict__ mag, int32_t* __restrict__ err) {
+                                                     const int32_t* __restrict__ dig_len, const int32_t* __restrict__ radix,
+                                                     u32 L, size_t count, u32* __restrict__ mag,
+                                                     int32_t* __restrict__ err) {
   const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= count * L) return;
   const size_t e = t / L;
   const u32 k = (u32)(t % L);
   const int64_t off = dig_off[e];
   const u32 len = (u32)dig_len[e];
-  u32 w = 0, bad = 0;
+  u32 bad = 0;
+  if (radix[e] == 10) {
+    if (k == 0) {
+      u64 v = 0;
+      for (u32 i = 0; i < len; ++i) {
+        const u32 ch = buf[off + i];
+        if (ch < '0' || ch > '9') { bad |= 1u; break; }
+        v = v * 10u + (ch - '0');
+      }
+      mag[e * L] = (u32)v;
+      if (L > 1) mag[e * L + 1] = (u32)(v >> 32);
+      else if (v >> 32) bad |= 2u;
+    } else if (k > 1) {
+      mag[e * L + k] = 0;
+    }
+    if (bad) atomicOr(err, (int32_t)bad);
+    return;
+  }
+  u32 w = 0;
   for (u32 i = 0; i < 8; ++i) {
     const u32 j = 8u * k + i;
     if (j >= len) break;
@@ -1459,21 +1509,22 @@ fphe_status fphe_import_signed(fphe_ctx* c, const uint32_t* mag, const uint8_t* 
 
 // ---- (8) wire format (see k_wire_encode) ----------------------------------------------
 fphe_status fphe_wire_lengths(const uint32_t* mag, const uint8_t* neg, uint32_t L, size_t count, int64_t* rec_len,
-                              void* stream) {
+                              uint8_t* radix, void* stream) {
   if (count == 0) return FPHE_OK;
-  if (!mag || !neg || !rec_len || L == 0) return FPHE_ERR_ARG;
+  if (!mag || !neg || !rec_len || !radix || L == 0) return FPHE_ERR_ARG;
   hipLaunchKernelGGL(k_wire_lengths, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, (hipStream_t)stream, mag,
-                     neg, L, count, rec_len);
+                     neg, L, count, rec_len, radix);
   return hip_ok(hipGetLastError());
 }
 
 fphe_status fphe_wire_encode(const uint32_t* mag, const uint8_t* neg, const int32_t* exp, uint32_t L, size_t count,
-                             const int64_t* rec_off, const int64_t* rec_len, uint8_t* out, void* stream) {
+                             const int64_t* rec_off, const int64_t* rec_len, const uint8_t* radix, uint8_t* out,
+                             void* stream) {
   if (count == 0) return FPHE_OK;
-  if (!mag || !neg || !exp || !rec_off || !rec_len || !out || L == 0) return FPHE_ERR_ARG;
+  if (!mag || !neg || !exp || !rec_off || !rec_len || !radix || !out || L == 0) return FPHE_ERR_ARG;
   const size_t threads = count * L;
   hipLaunchKernelGGL(k_wire_encode, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, (hipStream_t)stream, mag,
-                     neg, exp, L, count, rec_off, rec_len, out);
+                     neg, exp, L, count, rec_off, rec_len, radix, out);
   return hip_ok(hipGetLastError());
 }
 
@@ -1513,13 +1564,13 @@ fphe_status fphe_wire_scan(const uint8_t* buf, size_t nbytes, size_t pos, size_t
   return FPHE_OK;
 }
 
-fphe_status fphe_wire_decode(const uint8_t* buf, const int64_t* dig_off, const int32_t* dig_len, uint32_t L,
-                             size_t count, uint32_t* mag, int32_t* err, void* stream) {
+fphe_status fphe_wire_decode(const uint8_t* buf, const int64_t* dig_off, const int32_t* dig_len, const int32_t* radix,
+                             uint32_t L, size_t count, uint32_t* mag, int32_t* err, void* stream) {
   if (count == 0) return FPHE_OK;
-  if (!buf || !dig_off || !dig_len || !mag || !err || L == 0) return FPHE_ERR_ARG;
+  if (!buf || !dig_off || !dig_len || !radix || !mag || !err || L == 0) return FPHE_ERR_ARG;
   const size_t threads = count * L;
   hipLaunchKernelGGL(k_wire_decode, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, (hipStream_t)stream, buf,
-                     dig_off, dig_len, L, count, mag, err);
+                     dig_off, dig_len, radix, L, count, mag, err);
   return hip_ok(hipGetLastError());
 }
 

@@ -219,6 +219,65 @@ def _key_for(n: int, p: Optional[int] = None, q: Optional[int] = None) -> _KeyCt
         return k
 
 
+# ---- pickling helpers -------------------------------------------------------------------
+# The reference pickles every object as bincode bytes, returned by pyo3 as Vec<u8> (a list of
+# ints) and read back from any sequence of ints.  The state here is `bytes` (accepted by the
+# reference's __setstate__, which extracts Vec<u8> from any sequence; pickles 8x smaller than
+# a list); FPHE_PICKLE_STATE=list gives the reference's exact list form.
+_UNPICKLED = threading.local()
+
+
+def _pickle_state(b: bytes):
+    return list(b) if os.environ.get("FPHE_PICKLE_STATE") == "list" else b
+
+
+def _isqrt_exact(ns: int) -> Optional[int]:
+    import math
+    r = math.isqrt(ns)
+    return r if r * r == ns else None
+
+
+def _only_key_n(L2: int) -> Optional[int]:
+    """The modulus of the only key of this size in the process, else None."""
+    with _KEYS_LOCK:
+        ns = {n for (n, _), k in _KEYS.items() if k.L2 == L2}
+    return ns.pop() if len(ns) == 1 else None
+
+
+class unpickle_key:
+    """``with unpickle_key(pk): pickle.loads(...)`` -- the key a ciphertext vector's state is
+    read under (its signed integers become (C mod n^2, sign)).  Without it: the PK unpickled
+    last in this thread (a PHETensor pickles its PK before its data), else the only key of
+    the matching size in the process."""
+
+    def __init__(self, pk: "PK"):
+        self.n = pk.n
+
+    def __enter__(self):
+        self.prev = getattr(_UNPICKLED, "forced", None)
+        _UNPICKLED.forced = self.n
+        return self
+
+    def __exit__(self, *exc):
+        _UNPICKLED.forced = self.prev
+        return False
+
+
+def _unpickle_n(buf: bytes) -> int:
+    forced = getattr(_UNPICKLED, "forced", None)
+    if forced is not None:
+        return forced
+    last = getattr(_UNPICKLED, "n", None)
+    if last is not None:
+        return last
+    with _KEYS_LOCK:
+        ns = sorted({n for (n, _) in _KEYS})
+    if len(ns) == 1:
+        return ns[0]
+    raise TypeError("CiphertextVector state: no key to read it under (unpickle its PK first, or use "
+                    "fate_amd.paillier.unpickle_key(pk))")
+
+
 def _fit_limbs(v: "CiphertextVector", L2: int) -> "CiphertextVector":
     """Zero-extend / truncate limb rows to the key's L2 (exact for values < n^2; used for
     ``zeros()`` vectors, which are created before the key is known)."""
@@ -228,7 +287,7 @@ def _fit_limbs(v: "CiphertextVector", L2: int) -> "CiphertextVector":
         C = v.C[:, :L2, :].contiguous()
     else:
         C = torch.cat([v.C, v.C.new_zeros((v.C.shape[0], L2 - v.L2, WAVE))], dim=1)
-    return CiphertextVector(C, v.sign, v.exp, v.count)
+    return CiphertextVector(C, v.sign, v.exp, v.count, v.n)
 
 
 _ERR_MESSAGES = [
@@ -314,6 +373,16 @@ class PlaintextVector:
     def __str__(self):
         return f"PlaintextVector(len={self.count}, lp={self.lp})"
 
+    # pickling: the reference's state, bincode(PlaintextVector) (paillier.rs:395-402)
+    def __getstate__(self):
+        from . import wire
+        return _pickle_state(wire.plaintext_vector_to_bincode(self))
+
+    def __setstate__(self, state):
+        from . import wire
+        v = wire.plaintext_vector_from_bincode(bytes(state))
+        self.P, self.neg, self.exp, self.count = v.P, v.neg, v.exp, v.count
+
 
 class Plaintext:
     """Scalar plaintext (``fate_utils.paillier.Plaintext``): a length-1 vector."""
@@ -329,10 +398,13 @@ class CiphertextVector:
     C [ntiles, L2, 64] canonical residues mod n^2, sign (reference integer = C - n^2),
     exp (base-16 exponent)."""
 
-    __slots__ = ("C", "sign", "exp", "count")
+    # n: the key's modulus once known (set by encrypt and by every op that takes a PK);
+    # pickling needs it to write the reference's signed integers C - n^2
+    __slots__ = ("C", "sign", "exp", "count", "n")
 
-    def __init__(self, C: torch.Tensor = None, sign: torch.Tensor = None, exp: torch.Tensor = None, count: int = 0):
-        self.C, self.sign, self.exp, self.count = C, sign, exp, count
+    def __init__(self, C: torch.Tensor = None, sign: torch.Tensor = None, exp: torch.Tensor = None, count: int = 0,
+                 n: Optional[int] = None):
+        self.C, self.sign, self.exp, self.count, self.n = C, sign, exp, count, n
 
     # ---- construction / host views -----------------------------------------------
     @property
@@ -384,7 +456,7 @@ class CiphertextVector:
         C = torch.from_numpy(tiles.view(np.int32)).to(dev)
         sign = _pad_flat(torch.tensor([1 if c < 0 else 0 for c in cs], dtype=torch.uint8), count).to(dev)
         ex = _pad_flat(torch.tensor(list(exps), dtype=torch.int32), count).to(dev)
-        return CiphertextVector(C, sign, ex, count)
+        return CiphertextVector(C, sign, ex, count, _isqrt_exact(ns))
 
     def export_signed(self, pk: "PK") -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
         """The reference's signed integers on the device (fphe_export_signed): magnitudes as
@@ -410,15 +482,26 @@ class CiphertextVector:
                                                   _ptr(out.C), _ptr(out.sign), ctypes.c_void_p(_stream(dev))),
                    "fphe_import_signed")
         out.exp[:n] = exp.to(dev, torch.int32)
+        out.n = pk.n
         return out
 
-    # ---- pickling (wire format of this backend) ---------------------
+    # ---- pickling: the reference's state, bincode(CiphertextVector) (paillier.rs:219-226) --
     def __getstate__(self):
-        return {"C": self.C.cpu(), "sign": self.sign.cpu(), "exp": self.exp.cpu(), "count": self.count}
+        from . import wire
+        n = self.n if self.n is not None else _only_key_n(self.L2)
+        if n is None:
+            raise TypeError("CiphertextVector: key unknown (several keys of this size in the process); "
+                            "build it through a PK operation before pickling")
+        return _pickle_state(wire.ciphertext_vector_to_bincode(self, PK(n)))
 
-    def __setstate__(self, st):
-        dev = _device()
-        self.C, self.sign, self.exp, self.count = st["C"].to(dev), st["sign"].to(dev), st["exp"].to(dev), st["count"]
+    def __setstate__(self, state):
+        from . import wire
+        buf = bytes(state)
+        n = _unpickle_n(buf)
+        v, used = wire.ciphertext_vector_from_bincode(buf, PK(n))
+        if used != len(buf):
+            raise ValueError("bincode CiphertextVector: trailing bytes")
+        self.C, self.sign, self.exp, self.count, self.n = v.C, v.sign, v.exp, v.count, n
 
     # ---- element plumbing (torch indexing; no arithmetic) ---------------------------
     def _gather(self, idx: torch.Tensor) -> "CiphertextVector":
@@ -734,6 +817,37 @@ class CiphertextVector:
             self.C, self.sign, self.exp = r.C, r.sign, r.exp
         else:
             self._assign(torch.arange(0, r.count), r)
+
+
+def _keyed(fn):
+    """Stamp the key's modulus on the vectors an operation returns (and on an in-place
+    target that had none, e.g. a ``zeros()`` histogram): from its PK argument, else from
+    the input vector."""
+    import functools
+
+    @functools.wraps(fn)
+    def w(self, *args, **kw):
+        r = fn(self, *args, **kw)
+        pk = next((a for a in itertools.chain(args, kw.values()) if isinstance(a, PK)), None)
+        n = pk.n if pk is not None else self.n
+        if n is not None:
+            if self.n is None:
+                self.n = n
+            for v in (r if isinstance(r, list) else [r]):
+                if isinstance(v, CiphertextVector) and v.n is None:
+                    v.n = n
+                elif isinstance(v, Ciphertext) and v.vec.n is None:
+                    v.vec.n = n
+        return r
+    return w
+
+
+for _name in ("slice", "slice_indexes", "cat", "shuffle", "i_shuffle", "intervals_slice", "tolist", "add",
+              "add_scalar", "iadd", "idouble", "iadd_vec", "neg", "sub", "sub_scalar", "rsub", "rsub_scalar", "isub",
+              "isub_vec", "mul", "mul_scalar", "iadd_slice", "iadd_vec_self", "isub_vec_self", "iupdate",
+              "iupdate_with_masks", "chunking_cumsum_with_step", "intervals_sum_with_step", "pack_squeeze", "matmul",
+              "rmatmul", "_gather"):
+    setattr(CiphertextVector, _name, _keyed(getattr(CiphertextVector, _name)))
 
 
 class Ciphertext:
@@ -1067,18 +1181,23 @@ class PK:
                                         _ptr(rt), k.rng_key, k.next_nonce(), _ptr(out.C), _ptr(out.sign), stream),
                        "fphe_encrypt")
         out.exp[:n] = pv.exp[:n]
+        out.n = self.n
         return out
 
     def encrypt_encoded_scalar(self, plaintext: Plaintext, obfuscate: bool) -> Ciphertext:
         """``PK.encrypt_encoded_scalar`` (paillier.rs:58-60)."""
         return Ciphertext(self.encrypt_encoded(plaintext.vec, obfuscate))
 
+    # pickling: the reference's state, bincode(fixedpoint_paillier::PK) (paillier.rs:67-74)
     def __getstate__(self):
-        return {"n": self.n}
+        from . import wire
+        return _pickle_state(wire.pk_to_bincode(self))
 
-    def __setstate__(self, st):
+    def __setstate__(self, state):
+        from . import wire
         self._priv = None
-        self._init(st["n"])
+        self._init(wire.pk_from_bincode(bytes(state)).n)
+        _UNPICKLED.n = self.n  # the key of the ciphertext vectors that follow it in a pickle
 
 
 class SK:
@@ -1115,11 +1234,15 @@ class SK:
     def decrypt_to_encoded_scalar(self, data: Ciphertext) -> Plaintext:
         return Plaintext(self.decrypt_to_encoded(data.vec))
 
+    # pickling: bincode(fixedpoint_paillier::SK) (paillier.rs:91-98)
     def __getstate__(self):
-        return {"p": self.p, "q": self.q}
+        from . import wire
+        return _pickle_state(wire.sk_to_bincode(self))
 
-    def __setstate__(self, st):
-        self._init(st["p"], st["q"])
+    def __setstate__(self, state):
+        from . import wire
+        sk = wire.sk_from_bincode(bytes(state))
+        self._init(sk.p, sk.q)
 
 
 class Coder:
@@ -1134,11 +1257,14 @@ class Coder:
         self.max_int = n // MAX_INT_FRACTION
         self._key = _key_for(n)
 
+    # pickling: bincode(fixedpoint_paillier::Coder) (paillier.rs:128-135)
     def __getstate__(self):
-        return {"n": self.n}
+        from . import wire
+        return _pickle_state(wire.coder_to_bincode(self.n))
 
-    def __setstate__(self, st):
-        self._init(st["n"])
+    def __setstate__(self, state):
+        from . import wire
+        self._init(wire.coder_from_bincode(bytes(state)))
 
     # ---- vector encode (device) ------------------------------------------------------
     def _encode_float(self, arr, dtype: torch.dtype, device=None) -> PlaintextVector:
@@ -1315,6 +1441,12 @@ class Evaluator:
 
     @staticmethod
     def cat(vec_list: Sequence[CiphertextVector]) -> CiphertextVector:
+        out = Evaluator._cat(vec_list)
+        out.n = next((v.n for v in vec_list if v.n is not None), None)
+        return out
+
+    @staticmethod
+    def _cat(vec_list: Sequence[CiphertextVector]) -> CiphertextVector:
         vecs = [v for v in vec_list if v.count > 0]
         if not vecs:
             return CiphertextVector.zeros(0, vec_list[0].L2 if vec_list else 128)

@@ -6,8 +6,9 @@
 ``serialize`` is fixint little endian: ``i32`` = 4 bytes, a ``Vec`` or ``String`` = ``u64``
 length + items, structs and newtypes (``BInt``, ``CT``, ``PT``;
 ``math/src/rug/mod.rs:11``, ``paillier/src/lib.rs:7,47``) are their fields in order.  rug's
-serde support writes an ``Integer`` as the struct ``{radix: i32, value: String}``; this module
-writes radix 16 (lowercase digits, ``-`` for negatives) and reads any radix 2..36.
+serde support writes an ``Integer`` as the struct ``{radix: i32, value: String}`` with radix 10
+when the magnitude has at most 32 significant bits and 16 (lowercase) otherwise, ``-`` for
+negatives; this module writes the same and reads any radix 2..36.
 
 Parity status: the struct field order is read off the reference
 (``paillier/src/lib.rs:49-69``, ``fixedpoint_paillier/src/lib.rs:18-57,237-241,353-367``);
@@ -31,16 +32,33 @@ import torch
 from . import _lib
 from .paillier import (MAX_INT_FRACTION, CiphertextVector, PK, PlaintextVector, SK, _device, _ptr, _stream)
 
-RADIX = 16
 _DIGITS = "0123456789abcdefghijklmnopqrstuvwxyz"
+MIN_RECORD = 4 + 8 + 1 + 4  # radix, length, one digit, exponent
+
+
+def radix_of(v: int) -> int:
+    """rug's serde radix for an Integer: decimal up to 32 significant bits, else hex."""
+    return 10 if abs(v).bit_length() <= 32 else 16
 
 
 # ---- scalar big integers (keys, coders, plaintexts) ------------------------------------
 def bint(v: int) -> bytes:
-    """One rug ``Integer`` record: i32 radix | u64 len | ``-``? lowercase hex digits."""
-    s = format(v, "x") if v >= 0 else "-" + format(-v, "x")
-    b = s.encode("ascii")
-    return struct.pack("<iQ", RADIX, len(b)) + b
+    """One rug ``Integer`` record: i32 radix | u64 len | ``-``? digits (see radix_of)."""
+    r = radix_of(v)
+    digits = str(abs(v)) if r == 10 else format(abs(v), "x")
+    b = (("-" if v < 0 else "") + digits).encode("ascii")
+    return struct.pack("<iQ", r, len(b)) + b
+
+
+def parse_digits(txt: str, radix: int) -> int:
+    """rug-style digit string (optional leading ``-``, then digits of ``radix`` only) to an int;
+    ``ValueError`` for anything else (Python's int() would also accept ``_``, spaces, ``+``)."""
+    neg = txt.startswith("-")
+    body = txt[1:] if neg else txt
+    if not body or any(c not in _DIGITS[:radix] for c in body.lower()):
+        raise ValueError(f"bincode: {txt[:40]!r} is not a radix-{radix} integer")
+    v = int(body, radix)
+    return -v if neg else v
 
 
 class Reader:
@@ -66,8 +84,11 @@ class Reader:
         radix = self.i32()
         if not 2 <= radix <= 36:
             raise ValueError(f"bincode: Integer radix {radix} outside 2..36")
-        s = bytes(self._take(self.u64())).decode("ascii")
-        return int(s, radix)
+        try:
+            s = bytes(self._take(self.u64())).decode("ascii")
+        except UnicodeDecodeError as exc:
+            raise ValueError("bincode: non-ASCII Integer digits") from exc
+        return parse_digits(s, radix)
 
     def done(self) -> None:
         if self.pos != len(self.buf):
@@ -136,6 +157,8 @@ def plaintext_vector_to_bincode(pv: PlaintextVector) -> bytes:
 def plaintext_vector_from_bincode(buf: bytes, device=None) -> PlaintextVector:
     r = Reader(buf)
     n = r.u64()
+    if n > (len(buf) - 8) // MIN_RECORD:
+        raise ValueError("bincode PlaintextVector: element count larger than the buffer holds")
     sigs, exps = [], []
     for _ in range(n):
         sigs.append(r.bint())
@@ -158,14 +181,15 @@ def ciphertext_vector_to_bincode(cv: CiphertextVector, pk: PK) -> bytes:
     L = int(mag.shape[1])
     s = ctypes.c_void_p(_stream(dev))
     rec_len = torch.empty(n, dtype=torch.int64, device=dev)
-    _lib.check(lib.fphe_wire_lengths(_ptr(mag), _ptr(neg), L, n, _ptr(rec_len), s), "fphe_wire_lengths")
+    radix = torch.empty(n, dtype=torch.uint8, device=dev)
+    _lib.check(lib.fphe_wire_lengths(_ptr(mag), _ptr(neg), L, n, _ptr(rec_len), _ptr(radix), s), "fphe_wire_lengths")
     ends = torch.cumsum(rec_len, 0)
     total = int(ends[-1].item())
     rec_off = ends - rec_len
     out = torch.empty(total, dtype=torch.uint8, device=dev)
     exp = exp.to(torch.int32).contiguous()
-    _lib.check(lib.fphe_wire_encode(_ptr(mag), _ptr(neg), _ptr(exp), L, n, _ptr(rec_off), _ptr(rec_len), _ptr(out), s),
-               "fphe_wire_encode")
+    _lib.check(lib.fphe_wire_encode(_ptr(mag), _ptr(neg), _ptr(exp), L, n, _ptr(rec_off), _ptr(rec_len), _ptr(radix),
+                                    _ptr(out), s), "fphe_wire_encode")
     res = bytearray(8 + total)
     res[:8] = head
     torch.from_numpy(np.frombuffer(res, dtype=np.uint8)[8:]).copy_(out)  # D2H straight into the result
@@ -174,9 +198,9 @@ def ciphertext_vector_to_bincode(cv: CiphertextVector, pk: PK) -> bytes:
 
 def ciphertext_vector_from_bincode(buf: bytes, pk: PK, device=None) -> Tuple[CiphertextVector, int]:
     """Parse a ``CiphertextVector`` starting at ``buf[0]``; returns (vector, bytes consumed).
-    Radix-16 records are decoded on the device; any other radix (valid for rug, never written
-    by it for bincode here) is parsed on the host.  Raises ``ValueError`` on a malformed
-    record or a value with |c| >= n^2."""
+    Radix-16 records and radix-10 records of up to 19 digits (what rug writes) are decoded on
+    the device; any other radix (valid for rug's parser) is parsed on the host.  Raises
+    ``ValueError`` on a malformed record or a value with |c| >= n^2."""
     dev = _device(device)
     if len(buf) < 8:
         raise ValueError("bincode: truncated buffer")
@@ -184,6 +208,8 @@ def ciphertext_vector_from_bincode(buf: bytes, pk: PK, device=None) -> Tuple[Cip
     L = pk._key.L2
     if n == 0:
         return CiphertextVector.empty(0, L, dev), 8
+    if n > (len(buf) - 8) // MIN_RECORD:  # before sizing anything by an untrusted count
+        raise ValueError("bincode CiphertextVector: element count larger than the buffer holds")
     lib = _lib.load()
     raw = np.frombuffer(buf, dtype=np.uint8)
     dig_off = np.empty(n, dtype=np.int64)
@@ -201,19 +227,23 @@ def ciphertext_vector_from_bincode(buf: bytes, pk: PK, device=None) -> Tuple[Cip
     dbuf = torch.from_numpy(raw[:used].copy()).to(dev)
     mag = torch.zeros((n, L), dtype=torch.int32, device=dev)
     err = torch.zeros(1, dtype=torch.int32, device=dev)
-    hexrows = radix == 16
-    if hexrows.all():
+    on_device = (radix == 16) | ((radix == 10) & (dig_len <= 19))
+    if on_device.all():
         d_off = torch.from_numpy(dig_off).to(dev)  # held until the launch is queued
         d_len = torch.from_numpy(dig_len).to(dev)
-        _lib.check(lib.fphe_wire_decode(_ptr(dbuf), _ptr(d_off), _ptr(d_len), L, n, _ptr(mag), _ptr(err), s),
-                   "fphe_wire_decode")
+        d_rdx = torch.from_numpy(radix).to(dev)
+        _lib.check(lib.fphe_wire_decode(_ptr(dbuf), _ptr(d_off), _ptr(d_len), _ptr(d_rdx), L, n, _ptr(mag), _ptr(err),
+                                        s), "fphe_wire_decode")
     else:
         words = np.zeros((n, L), dtype=np.uint32)
         for e in range(n):
-            txt = bytes(raw[dig_off[e]: dig_off[e] + dig_len[e]]).decode("ascii")
-            v = int(txt, int(radix[e]))
-            if v.bit_length() > 32 * L:
-                raise ValueError("bincode CiphertextVector: value wider than n^2")
+            try:
+                txt = bytes(raw[dig_off[e]: dig_off[e] + dig_len[e]]).decode("ascii")
+            except UnicodeDecodeError as exc:
+                raise ValueError("bincode CiphertextVector: non-ASCII digits") from exc
+            v = parse_digits(txt, int(radix[e]))  # the sign was taken off by the scan
+            if v < 0 or v.bit_length() > 32 * L:
+                raise ValueError("bincode CiphertextVector: malformed value or wider than n^2")
             words[e] = np.frombuffer(v.to_bytes(4 * L, "little"), dtype=np.uint32)
         mag = torch.from_numpy(words.view(np.int32)).to(dev)
     if int(err.item()):

@@ -224,25 +224,28 @@ fphe_status fphe_import_signed(fphe_ctx* ctx, const uint32_t* mag, const uint8_t
  * structs whose big integers are rug::Integer, which rug's serde writes as {radix: i32,
  * value: String}.  Per element (fixedpoint_paillier Ciphertext / Plaintext, lib.rs:237-241,
  * 358-362): i32 radix | u64 len | "-"? digits | i32 exp; a vector is u64 count + elements
- * (CiphertextVector.__getstate__ / __setstate__, paillier.rs:219-226).  Radix 16 lowercase
- * is written.  The byte layout follows rug 1.20's published serde code and is not pinned
- * against a real rug build (none in this image).  No context: pure data formatting.
- *   fphe_wire_lengths: rec_len[e] = bytes of element e's record (device).
+ * (CiphertextVector.__getstate__ / __setstate__, paillier.rs:219-226).  The radix follows
+ * rug 1.20's serde: 10 for magnitudes of at most 32 significant bits, else 16 (lowercase).
+ * The byte layout follows rug's published serde code and is not pinned against a real rug
+ * build (none in this image).  No context: pure data formatting.
+ *   fphe_wire_lengths: rec_len[e] = bytes of element e's record, radix[e] = 10 or 16 (device).
  *   fphe_wire_encode:  records at out + rec_off[e] (device; rec_off = exclusive scan of
  *                      the rec_len that fphe_wire_lengths wrote for the same mag / neg).
  *   fphe_wire_scan:    HOST walk of `count` records from buf + pos: digit offsets/lengths,
  *                      sign, exp, radix per element; *end = offset after the last record.
  *                      FPHE_ERR_ARG on a truncated record or a radix outside 2..36.
- *   fphe_wire_decode:  radix-16 digit strings -> mag[count][L] (device); err |= 1 for a
- *                      non-hex digit, 2 for a value wider than L words. */
+ *   fphe_wire_decode:  radix-16 digit strings, and radix-10 ones of at most 19 digits, ->
+ *                      mag[count][L] (device); err |= 1 for a character that is not a digit
+ *                      of the radix, 2 for a value wider than L words. */
 fphe_status fphe_wire_lengths(const uint32_t* mag, const uint8_t* neg, uint32_t L, size_t count, int64_t* rec_len,
-                              void* stream);
+                              uint8_t* radix, void* stream);
 fphe_status fphe_wire_encode(const uint32_t* mag, const uint8_t* neg, const int32_t* exp, uint32_t L, size_t count,
-                             const int64_t* rec_off, const int64_t* rec_len, uint8_t* out, void* stream);
+                             const int64_t* rec_off, const int64_t* rec_len, const uint8_t* radix, uint8_t* out,
+                             void* stream);
 fphe_status fphe_wire_scan(const uint8_t* buf, size_t nbytes, size_t pos, size_t count, int64_t* dig_off,
                            int32_t* dig_len, uint8_t* neg, int32_t* exp, int32_t* radix, size_t* end);
-fphe_status fphe_wire_decode(const uint8_t* buf, const int64_t* dig_off, const int32_t* dig_len, uint32_t L,
-                             size_t count, uint32_t* mag, int32_t* err, void* stream);
+fphe_status fphe_wire_decode(const uint8_t* buf, const int64_t* dig_off, const int32_t* dig_len, const int32_t* radix,
+                             uint32_t L, size_t count, uint32_t* mag, int32_t* err, void* stream);
 
 /* Known-answer hook for the device CSPRNG behind the obfuscation nonces (fphe_encrypt with
  * r == NULL draws r from ChaCha20, chacha_dev.h; the reference's r comes from

@@ -1,7 +1,8 @@
 """Wire format of the reference's pickles (fate_amd/wire.py; bincode(serde) of
 fate_utils.paillier objects, paillier.rs:67-74,91-98,128-135,219-226,395-402).  The rug
 Integer record layout is unpinned (no rug / bincode in this image): these tests pin the
-layout as documented in include/fate_phe.h (8) and check device encode/decode against a
+layout as documented in include/fate_phe.h (8) -- rug's serde radix rule included: decimal
+up to 32 significant bits, lowercase hex above -- and check device encode/decode against a
 record-by-record construction written here from the spec, plus round trips."""
 import json
 import os
@@ -22,8 +23,11 @@ def fixture(bits):
         return json.load(f)
 
 
-def rec(v, radix=16):
-    """One rug Integer record built from the spec: i32 radix, u64 len, sign + digits."""
+def rec(v, radix=None):
+    """One rug Integer record built from the spec: i32 radix, u64 len, sign + digits; the
+    radix rug's serde picks unless one is given."""
+    if radix is None:
+        radix = 10 if abs(v).bit_length() <= 32 else 16
     digs = "0123456789abcdefghijklmnopqrstuvwxyz"
     m, out = abs(v), ""
     while True:
@@ -35,21 +39,35 @@ def rec(v, radix=16):
     return struct.pack("<i", radix) + struct.pack("<Q", len(s)) + s.encode()
 
 
-def ct_vec_bytes(cs, es, radix=16):
+def ct_vec_bytes(cs, es, radix=None):
     return struct.pack("<Q", len(cs)) + b"".join(rec(c, radix) + struct.pack("<i", e) for c, e in zip(cs, es))
 
 
 def test_bint_records():
-    assert wire.bint(0) == struct.pack("<iQ", 16, 1) + b"0"
-    assert wire.bint(-255) == struct.pack("<iQ", 16, 3) + b"-ff"
-    for v in (1, -1, 2**64, -(2**4095 + 12345), 0xDEADBEEF):
+    assert wire.bint(0) == struct.pack("<iQ", 10, 1) + b"0"
+    assert wire.bint(-255) == struct.pack("<iQ", 10, 4) + b"-255"
+    assert wire.bint(2**32 - 1) == struct.pack("<iQ", 10, 10) + b"4294967295"  # 32 bits: decimal
+    assert wire.bint(2**32) == struct.pack("<iQ", 16, 9) + b"100000000"        # 33 bits: hex
+    assert wire.bint(-(2**40)) == struct.pack("<iQ", 16, 12) + b"-10000000000"
+    for v in (1, -1, 2**64, -(2**4095 + 12345), 0xDEADBEEF, 2**31, -(2**32) + 1):
         assert wire.bint(v) == rec(v)
         assert wire.Reader(rec(v)).bint() == v
         assert wire.Reader(rec(v, 10)).bint() == v  # any radix reads back
+        assert wire.Reader(rec(v, 36)).bint() == v
     with pytest.raises(ValueError):
         wire.Reader(rec(5)[:-1]).bint()
     with pytest.raises(ValueError):
         wire.Reader(struct.pack("<iQ", 40, 1) + b"1").bint()
+    for bad in (b"--5", b"1_0", b" 7", b"+7", b"", b"-", b"12a"):  # int() would take some of these
+        with pytest.raises(ValueError):
+            wire.Reader(struct.pack("<iQ", 10, len(bad)) + bad).bint()
+
+
+def test_untrusted_counts_rejected_before_allocation():
+    """A vector header claiming more elements than the bytes can hold is a ValueError, not
+    an allocation sized by the untrusted count."""
+    with pytest.raises(ValueError):
+        wire.plaintext_vector_from_bincode(struct.pack("<Q", 2**60) + b"x" * 40)
 
 
 def test_key_and_coder_records():
@@ -79,7 +97,7 @@ def test_scan_walks_records():
     """fphe_wire_scan (host code in the C ABI library): offsets, signs, exps, radixes."""
     lib = _lib.load()
     cs, es = [0, -5, 2**100 + 7, 255], [-14, 3, 0, -2**31]
-    buf = ct_vec_bytes(cs[:2], es[:2]) + ct_vec_bytes(cs[2:], es[2:], radix=10)[8:]
+    buf = ct_vec_bytes(cs[:2], es[:2], radix=16) + ct_vec_bytes(cs[2:], es[2:], radix=10)[8:]
     raw = np.frombuffer(buf, dtype=np.uint8)
     n = len(cs)
     off, ln = np.empty(n, np.int64), np.empty(n, np.int32)
@@ -127,8 +145,19 @@ def test_ciphertext_vector_device_codec(bits, count):
 @pytest.mark.gpu
 def test_ciphertext_vector_decode_other_radix_and_errors():
     pk, cv, cs, es = _dev_cts(1024, 40, 1)
-    back, _ = wire.ciphertext_vector_from_bincode(ct_vec_bytes(cs, es, radix=10), pk)
+    back, _ = wire.ciphertext_vector_from_bincode(ct_vec_bytes(cs, es, radix=10), pk)  # long decimal: host
     assert back.to_signed_ints(pk.ns) == (cs, es)
+    back, _ = wire.ciphertext_vector_from_bincode(ct_vec_bytes(cs, es, radix=16), pk)  # all hex: device
+    assert back.to_signed_ints(pk.ns) == (cs, es)
+    small = [0, 1, -7, 2**32 - 1, 2**33, -(2**32 - 1), 10**18]  # <= 19 decimal digits: device
+    back, _ = wire.ciphertext_vector_from_bincode(ct_vec_bytes(small, [0] * 7, radix=10), pk)
+    assert back.to_signed_ints(pk.ns) == (small, [0] * 7)
+    with pytest.raises(ValueError):  # a non-decimal character in a decimal record (device path)
+        wire.ciphertext_vector_from_bincode(struct.pack("<QiQ", 1, 10, 3) + b"1a2" + struct.pack("<i", 0), pk)
+    with pytest.raises(ValueError):  # doubled sign (host path: radix 7)
+        wire.ciphertext_vector_from_bincode(struct.pack("<QiQ", 1, 7, 3) + b"--5" + struct.pack("<i", 0), pk)
+    with pytest.raises(ValueError):  # more elements claimed than the buffer holds
+        wire.ciphertext_vector_from_bincode(struct.pack("<Q", 2**40) + b"\0" * 64, pk)
     up = ct_vec_bytes(cs, es).replace(b"a", b"A")  # uppercase hex digits are accepted
     assert wire.ciphertext_vector_from_bincode(up, pk)[0].to_signed_ints(pk.ns) == (cs, es)
     with pytest.raises(ValueError):  # |c| >= n^2
@@ -150,3 +179,89 @@ def test_plaintext_vector_codec():
     b = wire.plaintext_vector_to_bincode(pv)
     assert b == ct_vec_bytes(sigs, exps)
     assert wire.plaintext_vector_from_bincode(b).to_ints() == (sigs, exps)
+
+
+def test_pickle_state_is_the_reference_bincode():
+    """PK / SK / Coder pickle as the reference does (paillier.rs:67-74, 91-98, 128-135): the
+    state is bincode(serde(...)), and __setstate__ takes it back as bytes or as the list of
+    ints pyo3 makes of a Vec<u8>."""
+    import pickle
+    fx = fixture(1024)
+    p, q = int(fx["p"], 16), int(fx["q"], 16)
+    sk, pk, coder = P.keypair_from_primes(p, q)
+    assert pk.__getstate__() == wire.pk_to_bincode(pk)
+    assert sk.__getstate__() == wire.sk_to_bincode(sk)
+    assert coder.__getstate__() == wire.coder_to_bincode(pk.n)
+    for obj in (pk, sk, coder):
+        back = pickle.loads(pickle.dumps(obj))
+        assert type(back) is type(obj) and back.__getstate__() == obj.__getstate__()
+        fresh = type(obj).__new__(type(obj))
+        fresh.__setstate__(list(obj.__getstate__()))  # pyo3's Vec<u8> form
+        assert fresh.__getstate__() == obj.__getstate__()
+    assert pickle.loads(pickle.dumps(pk)).keyholder is False  # a pickled PK is public-only
+
+
+def test_fate_utils_alias_passes_the_federation_allowlist():
+    """compat.install(): the classes pickle under fate_utils.paillier, which FATE's restricted
+    unpickler admits (arch/federation/api/_serdes.py:280, 311-333: module prefixes "fate." and
+    "fate_utils." only), and FATE's adapter imports resolve (protocol/phe/paillier.py:18-23)."""
+    import io
+    import pickle
+    import subprocess
+    import sys
+    code = r'''
+import io, pickle, sys, json
+sys.path.insert(0, %r)
+from fate_amd import compat
+mod = compat.install()
+from fate_utils.paillier import CiphertextVector, PlaintextVector, Coder, Evaluator, PK, SK, keygen  # noqa
+fx = json.load(open(%r))
+import fate_amd.paillier as P
+p, q = int(fx["p"], 16), int(fx["q"], 16)
+sk, pk, _ = P.keypair_from_primes(p, q)
+coder = Coder(p * q)
+class Restricted(pickle.Unpickler):
+    def find_class(self, module, name):
+        if not any(module.startswith(m) for m in ("fate.", "fate_utils.")):
+            raise pickle.UnpicklingError(module)
+        return super().find_class(module, name)
+out = []
+for obj in (pk, sk, coder):
+    b = pickle.dumps(obj)
+    assert b"fate_utils.paillier" in b and b"fate_amd" not in b, b[:80]
+    back = Restricted(io.BytesIO(b)).load()
+    out.append(type(back).__module__ + "." + type(back).__name__)
+assert compat.install() is mod
+print(json.dumps(out))
+''' % (os.path.dirname(HERE), os.path.join(HERE, "golden", "paillier_1024.json"))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert json.loads(r.stdout.strip().splitlines()[-1]) == ["fate_utils.paillier.PK", "fate_utils.paillier.SK",
+                                                             "fate_utils.paillier.Coder"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", [1024, 2048])
+def test_ciphertext_and_plaintext_vector_pickle(bits):
+    """CiphertextVector / PlaintextVector pickle through the reference's bincode state
+    (paillier.rs:219-226, 395-402), read back under the key of the PK unpickled before them
+    (a PHETensor pickles its PK first) or under fate_amd.paillier.unpickle_key."""
+    import pickle
+    pk, cv, cs, es = _dev_cts(bits, 300, 7)
+    assert cv.__getstate__() == wire.ciphertext_vector_to_bincode(cv, pk) == ct_vec_bytes(cs, es)
+    pk2, back = pickle.loads(pickle.dumps((pk, cv)))
+    assert back.to_signed_ints(pk.ns) == (cs, es) and back.n == pk.n
+    with P.unpickle_key(pk):
+        again = pickle.loads(pickle.dumps(cv))
+    assert again.to_signed_ints(pk.ns) == (cs, es)
+    fresh = P.CiphertextVector.__new__(P.CiphertextVector)
+    with P.unpickle_key(pk):
+        fresh.__setstate__(list(cv.__getstate__()))  # pyo3's Vec<u8> form
+    assert fresh.to_signed_ints(pk.ns) == (cs, es)
+    # ops stamp the key: an encryption's sums pickle without help
+    x = torch.linspace(-3, 3, 70, device="cuda")
+    e = pk.encrypt_encoded(P.Coder(pk.n).encode_f32_vec(x), True)
+    s = e.add(pk, e)
+    assert s.n == pk.n and pickle.loads(pickle.dumps((pk, s)))[1].to_signed_ints(pk.ns) == s.to_signed_ints(pk.ns)
+    pv = P.PlaintextVector.from_ints([0, -3, 2**60 + 1], [-14, 2, 0])
+    assert pickle.loads(pickle.dumps(pv)).to_ints() == pv.to_ints()
