@@ -157,6 +157,67 @@ def cpu_baseline(p: int, q: int, seconds: float = 3.0):
     }
 
 
+def valu_roofline(kernel: str, mac32: float, ms: float, hbm_bytes: float, **extra) -> dict:
+    """A roofline block in SURVEY.md §8(d)'s MAC32 accounting for one timed launch."""
+    achieved = mac32 / (ms / 1e3) / 1e12
+    return {"bound": "valu", "kernel": kernel, "achieved": round(achieved, 3), "peak": round(PEAK_TMAC32, 3),
+            "unit": "TMAC32/s", "frac": round(achieved / PEAK_TMAC32, 4), "kernel_ms": round(ms, 3),
+            "hbm": {"achieved": round(hbm_bytes / (ms / 1e3) / 1e9, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s"},
+            **extra}
+
+
+def add_kernel_leg(P, pk, a, b, N, stream, dev) -> dict:
+    """The ct-add kernel alone (k_add27 through fphe_add_ordered, launched on `stream`) on the
+    Hetero-LR-shaped operands, in the exponent-gap order _add computes.  §8(d): an aligned
+    add is one mulmod over L = 128 32-bit limbs (32,896 MAC32); each step of exponent gap
+    adds 4 squarings of the same size (decrese_exp_to, fixedpoint_paillier/src/lib.rs:
+    250-258); literal-1 operands cost nothing.  Algorithmic HBM bytes: two operands read,
+    one result written, 517 B each (+ the 4-B order entry)."""
+    import ctypes
+    from fate_amd import _lib
+    gaps = (a.exp[:N] - b.exp[:N]).abs()
+    order = P._add_order(a.exp[:N], b.exp[:N], a.L2)
+    out = P.CiphertextVector.empty(N, a.L2, dev)
+    lib = _lib.load()
+    ctx = pk._key.ctx(dev)
+
+    def launch():
+        _lib.check(lib.fphe_add_ordered(ctx, P._ptr(a.C), P._ptr(a.sign), P._ptr(a.exp), P._ptr(b.C), P._ptr(b.sign),
+                                        P._ptr(b.exp), 1, N, P._ptr(order), P._ptr(out.C), P._ptr(out.sign),
+                                        P._ptr(out.exp), ctypes.c_void_p(stream.cuda_stream)), "fphe_add_ordered")
+
+    launch()  # warm-up
+    ev = []
+    for _ in range(3):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        launch()
+        e1.record(stream)
+        ev.append((e0, e1))
+    torch.cuda.synchronize(dev)
+    ms = sum(x.elapsed_time(y) for x, y in ev) / len(ev)
+    L = a.L2
+    mac = N * (1 + 4 * float(gaps.double().mean())) * mac32_per_mont(L)
+    hist = torch.bincount(gaps.cpu()).tolist()
+    # issued 27-bit MACs: to-Montgomery + final product (general) and the wave-max squarings
+    NL = 38 * (L // 32)
+    TPI = NL // 38
+    per_wave = 64 // TPI
+    gs = gaps[order.long()] if order is not None else gaps
+    pad = (-N) % per_wave
+    if pad:
+        gs = torch.cat([gs, gs.new_zeros(pad)])
+    wave_sq = 4 * gs.view(-1, per_wave).amax(1).double().sum().item() * per_wave
+    mads = N * 2 * 2 * NL * NL + wave_sq * NL * TPI * (20 + 38)
+    blk = valu_roofline("k_add27<128> (exponent-gap order)", mac, ms, N * (3 * (L * 4 + 5) + 4),
+                        per_elem_mac32=round(mac / N, 1), gap_histogram=hist, sorted=order is not None)
+    blk["issue"] = {"mad64_per_elem": round(mads / N, 1), "achieved": round(mads / (ms / 1e3) / 1e12, 3),
+                    "peak": round(PEAK_TMAC32, 3), "unit": "Tmad/s",
+                    "frac": round(mads / (ms / 1e3) / 1e12 / PEAK_TMAC32, 4)}
+    return blk
+
+
 def hist_packed_leg(P, pk, sk, coder, N, HF, NB, key_bits, rank, dev):
     """SecureBoost histogram on the reference's default gh-packed path (BASELINE config 4
     (ii); ml/ensemble/learner/decision_tree/hetero/guest.py:195-235, binary task): the guest
@@ -255,8 +316,11 @@ def launch_ranks(nproc: int) -> int:
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
+    # torchrun's own parser would take "--n" as an abbreviation of its options: pass --elements
+    args = ["--elements" if a == "--n" else ("--elements=" + a[4:] if a.startswith("--n=") else a)
+            for a in sys.argv[1:]]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
-           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + args
     return subprocess.call(cmd)
 
 
@@ -405,6 +469,7 @@ def main() -> None:
         e1.record(stream)
         torch.cuda.synchronize(dev)
         add_ms = e0.elapsed_time(e1)
+        add_kernel = add_kernel_leg(P, pk, ct, ct2, N, stream, dev)
         # end-to-end from host f32 to host ciphertexts (pinned), one pass
         xh = x.pin_memory()
         torch.cuda.synchronize(dev)
@@ -542,6 +607,12 @@ def main() -> None:
             "e2e_host_encrypts_per_s": round(N / e2e, 1),
             "roundtrip_bit_exact": roundtrip_ok,
             "decrypt_roofline_frac": round(N * dec_mac32_per_elem(key_bits) / (dec_ms / 1e3) / 1e12 / PEAK_TMAC32, 4),
+            "rooflines": {
+                "decrypt": valu_roofline("k_pow_half27<128,6,false> + k_decrypt_crt<128>",
+                                         N * dec_mac32_per_elem(key_bits), dec_ms,
+                                         N * (key_bits // 4 + 4 + key_bits // 8)),
+                "ct_add": add_kernel,
+            },
         }
         del pt, y, ct2, s, ce, Ch, m, gh, hist
 

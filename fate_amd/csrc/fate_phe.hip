@@ -142,8 +142,12 @@ __device__ __forceinline__ bool nude_to_slot(u32* slot, const KeyArgs& K, const 
 template <int L1>
 __device__ __forceinline__ void draw_r(u32 (&A)[L1], const KeyArgs& K, const ChaChaKey& ck, u64 nonce, size_t e) {
   constexpr int NB = (L1 + 15) / 16;
-  const int topbits = K.nbits - 32 * (L1 - 1);
-  const u32 topmask = topbits >= 32 ? 0xffffffffu : ((1u << topbits) - 1u);
+  // keep bits(n) random bits: words past the top of n (keys narrower than the L1-word
+  // geometry) are 0, the top word is masked
+  auto wmask = [&](int j) -> u32 {
+    const int b = K.nbits - 32 * j;
+    return b >= 32 ? 0xffffffffu : (b <= 0 ? 0u : ((1u << b) - 1u));
+  };
   bool done = false;
   u32 attempt = 0;
   while (__any(!done)) {
@@ -160,7 +164,8 @@ __device__ __forceinline__ void draw_r(u32 (&A)[L1], const KeyArgs& K, const Cha
         for (int i = 0; i < 16; ++i)
           if (b * 16 + i < L1) x[b * 16 + i] = blk[i];
       }
-      x[L1 - 1] &= topmask;
+#pragma unroll
+      for (int j = 0; j < L1; ++j) x[j] &= wmask(j);
       // accept iff x < n - 1, then r = x + 1 in [1, n-1]  (random.rs:22-25)
       u32 br = 0;
 #pragma unroll
@@ -1039,9 +1044,12 @@ extern "C" {
 fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, const uint32_t* p_w,
                             const uint32_t* q_w, fphe_ctx** out) {
   if (!out || !n_w) return FPHE_ERR_ARG;
-  if (key_bits != 1024 && key_bits != 2048) return FPHE_ERR_ARG;
+  // any even size up to 2048 bits (paillier/src/lib.rs:72-87 accepts any even size): the
+  // kernels run the 1024- or the 2048-bit geometry with n zero-padded to it (R >= 4N holds,
+  // so the lazy Montgomery bounds are unchanged)
+  if (key_bits < 256 || key_bits > 2048 || key_bits % 2) return FPHE_ERR_ARG;
   if ((p_w == nullptr) != (q_w == nullptr)) return FPHE_ERR_ARG;
-  const int L1 = key_bits / 32, L2 = 2 * L1, LQ = L1 / 2;
+  const int L1 = key_bits <= 1024 ? 32 : 64, L2 = 2 * L1, LQ = L1 / 2;
   try {
     Limbs n = from_words(n_w, L1);
     if (n.empty() || !(n[0] & 1)) return FPHE_ERR_KEY;

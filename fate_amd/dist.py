@@ -34,9 +34,9 @@ def shard_bounds(count: int, rank: int, world: int) -> Tuple[int, int]:
 def gather_tiles(C: torch.Tensor, sign: torch.Tensor, exp: torch.Tensor, count: int, group=None,
                  trim: bool = True):
     """All-gather the per-rank shards (tile-major C [nt, L, 64], sign/exp [nt*64]) into the
-    full vector on every rank.  Shards are padded to the largest shard for the collective
-    and, with ``trim``, the padding tiles are cut out after (one copy of the gathered
-    vector).  Returns (C, sign, exp, total_count); with ``trim=False`` the padded buffers
+    full vector on every rank, elements in rank order.  Shards are padded to the largest
+    shard for the collective and, with ``trim``, the padding is cut out after (one copy of
+    the gathered vector; ragged shards by an element gather).  Returns (C, sign, exp, total_count); with ``trim=False`` the padded buffers
     as gathered ([world * nt_max] tiles, rank r's shard at tiles [r * nt_max, ...)) and the
     per-rank counts instead of the total."""
     import torch.distributed as dist
@@ -74,18 +74,31 @@ def gather_tiles(C: torch.Tensor, sign: torch.Tensor, exp: torch.Tensor, count: 
     dist.all_gather_into_tensor(eg, pad_flat(exp), group=group)
     if not trim:
         return Cg, sg, eg, counts
+    total = sum(counts)
     if all(c == nt_max * WAVE for c in counts[:-1]) and (counts[-1] + WAVE - 1) // WAVE == nt_max:
         # no padding tiles (only the last shard's partial tile, which is the vector's end)
-        return Cg, sg.to(torch.uint8), eg, sum(counts)
-    # shards are whole tiles except possibly the last rank's: drop the per-rank padding
-    Cs, ss, es = [], [], []
-    for r, c in enumerate(counts):
-        nt = (c + WAVE - 1) // WAVE
-        Cs.append(Cg[r * nt_max: r * nt_max + nt])
-        ss.append(sg[r * nt_max * WAVE: r * nt_max * WAVE + nt * WAVE])
-        es.append(eg[r * nt_max * WAVE: r * nt_max * WAVE + nt * WAVE])
-    total = sum(counts)
-    return torch.cat(Cs), torch.cat(ss).to(torch.uint8), torch.cat(es), total
+        return Cg, sg.to(torch.uint8), eg, total
+    if all(c % WAVE == 0 for c in counts[:-1]):
+        # whole-tile shards (shard_bounds): drop the per-rank padding tiles
+        Cs, ss, es = [], [], []
+        for r, c in enumerate(counts):
+            nt = (c + WAVE - 1) // WAVE
+            Cs.append(Cg[r * nt_max: r * nt_max + nt])
+            ss.append(sg[r * nt_max * WAVE: r * nt_max * WAVE + nt * WAVE])
+            es.append(eg[r * nt_max * WAVE: r * nt_max * WAVE + nt * WAVE])
+        return torch.cat(Cs), torch.cat(ss).to(torch.uint8), torch.cat(es), total
+    # ragged shards (e.g. per-rank partial histograms of any slot count): element gather of
+    # the valid slots, rank r's element k sitting at r * nt_max * 64 + k of the gathered tiles
+    idx = torch.cat([torch.arange(c, device=dev) + r * nt_max * WAVE for r, c in enumerate(counts)])
+    rows = Cg.permute(0, 2, 1).reshape(-1, L)[idx]
+    nt = (total + WAVE - 1) // WAVE
+    Cf = rows.new_zeros((nt * WAVE, L))
+    Cf[:total] = rows
+    sf = sg.new_zeros(nt * WAVE)
+    sf[:total] = sg[idx]
+    ef = eg.new_zeros(nt * WAVE)
+    ef[:total] = eg[idx]
+    return Cf.view(nt, WAVE, L).permute(0, 2, 1).contiguous(), sf.to(torch.uint8), ef, total
 
 
 def gather_ciphertexts(cv, group=None):

@@ -161,15 +161,27 @@ def _pad_flat(x: torch.Tensor, n: int) -> torch.Tensor:
 # --------------------------------------------------------------------------------------
 # per-device key contexts
 # --------------------------------------------------------------------------------------
+MIN_KEY_BITS, MAX_KEY_BITS = 256, 2048
+
+
+def supports(key_bits: int) -> bool:
+    """Key sizes this backend runs: even, MIN_KEY_BITS..MAX_KEY_BITS.  The reference takes any
+    even size (paillier/src/lib.rs:72-87); FATE's integration keeps its CPU path for the
+    others (INTEGRATION.md)."""
+    return MIN_KEY_BITS <= key_bits <= MAX_KEY_BITS and key_bits % 2 == 0
+
+
 class _KeyCtx:
     """Owns one fphe_ctx per HIP device for a key (public, or public+private)."""
 
     def __init__(self, n: int, p: Optional[int] = None, q: Optional[int] = None):
         self.n, self.p, self.q = n, p, q
         self.key_bits = n.bit_length()
-        if self.key_bits not in (1024, 2048):
-            raise ValueError(f"unsupported key size {self.key_bits} (1024 or 2048)")
-        self.L1 = self.key_bits // 32
+        if not supports(self.key_bits):
+            raise ValueError(f"unsupported key size {self.key_bits}: this backend runs even sizes "
+                             f"{MIN_KEY_BITS}..{MAX_KEY_BITS} (larger keys stay on the CPU fate_utils path)")
+        # geometry: the 1024- or 2048-bit kernels, n zero-padded up to it
+        self.L1 = 32 if self.key_bits <= 1024 else 64
         self.L2 = 2 * self.L1
         self._ctx: Dict[int, ctypes.c_void_p] = {}
         self._lock = threading.Lock()
@@ -886,7 +898,9 @@ def _add_order(ea: torch.Tensor, eb: torch.Tensor, L2: int) -> Optional[torch.Te
             x = torch.cat([x, x.new_zeros(pad)])
         return (2 + 4 * x.view(-1, per_wave).amax(1)).sum()
 
-    ds, order = torch.sort(d, stable=True)
+    # largest gaps first: the few long waves (a 0.0 against a large value can differ by 30
+    # exponent steps, 120 squarings) start at the head of the grid instead of trailing it
+    ds, order = torch.sort(d, stable=True, descending=True)
     c = torch.stack([cost(d), cost(ds)]).tolist()
     if c[1] > 0.95 * c[0]:
         return None
@@ -1475,7 +1489,11 @@ class Evaluator:
 
 
 def keygen(bit_length: int) -> Tuple[SK, PK, Coder]:
-    """``fate_utils.paillier.keygen`` (paillier.rs:206-210; fixedpoint_paillier::keygen lib.rs:408-413)."""
+    """``fate_utils.paillier.keygen`` (paillier.rs:206-210; fixedpoint_paillier::keygen lib.rs:408-413).
+    Odd sizes fail as the reference's assert does; even sizes outside :func:`supports` raise
+    ``ValueError`` before any key is drawn."""
+    if bit_length % 2 == 0 and not supports(bit_length):
+        raise ValueError(f"unsupported key size {bit_length}: even {MIN_KEY_BITS}..{MAX_KEY_BITS} run on MI355X")
     p, q = keygen_primes(bit_length)
     return SK(p, q), PK(p * q)._bind_private(p, q), Coder(p * q)
 

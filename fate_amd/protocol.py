@@ -158,8 +158,15 @@ class Coder:
         return torch.tensor(self.coder.decode_i32_vec(vec))
 
 
+def supports(key_size: int) -> bool:
+    """Whether this backend runs keys of ``key_size`` bits (even, 256..2048).  The
+    ``PHECipherBuilder.setup`` branch in INTEGRATION.md keeps FATE's CPU module for the rest
+    (the reference accepts any even size, paillier/src/lib.rs:72-87)."""
+    return _p.supports(key_size)
+
+
 def keygen(key_size):
-    """paillier.py:174-176."""
+    """paillier.py:174-176.  ValueError for sizes :func:`supports` rejects."""
     sk, pk, coder = _p.keygen(key_size)
     return SK(sk), PK(pk), Coder(coder)
 

@@ -16,7 +16,8 @@
  *    its 64 elements as one 256-byte row.  Per-element byte/int arrays (sign, neg,
  *    exp) are flat [T*64].  Buffers are padded to whole tiles.
  *  - A ciphertext vector is (C, sign, exp):
- *      C    : uint32 [T][L2][64]   canonical residue in [0, n^2), L2 = key_bits/16
+ *      C    : uint32 [T][L2][64]   canonical residue in [0, n^2), L2 = 64 for keys of at
+ *                                  most 1024 bits, 128 up to 2048 (fphe_ctx_limbs)
  *      sign : uint8  [T*64]        1 iff the reference's signed integer is C - n^2
  *      exp  : int32  [T*64]        base-16 fixed-point exponent
  *    The reference keeps ciphertexts as signed rug::Integer values because rug's
@@ -59,9 +60,11 @@ typedef struct fphe_ctx fphe_ctx;
 /* Create a device context for one Paillier key on HIP device `device`.
  * Replaces the key objects behind fate_utils.paillier.PK / SK
  * (paillier.rs:18-24; crates/paillier/src/lib.rs:49-69, SK::new :125-150).
- *   n      : key_bits/32 limbs (little-endian uint32), the public modulus.
- *   p, q   : key_bits/64 limbs each, or both NULL for a public-only context.
- * key_bits must be 1024 or 2048. */
+ *   n      : L1 limbs (little-endian uint32, zero-padded), the public modulus, bits(n) ==
+ *            key_bits (paillier/src/lib.rs:82); L1 = 32 for key_bits <= 1024, else 64.
+ *   p, q   : L1/2 limbs each (zero-padded), or both NULL for a public-only context.
+ * key_bits: any even size 256..2048 (the reference takes any even size, lib.rs:72-87).
+ * Keys below the geometry's width run its kernels with zero-padded limbs. */
 fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n,
                             const uint32_t* p, const uint32_t* q, fphe_ctx** out);
 fphe_status fphe_ctx_destroy(fphe_ctx* ctx);

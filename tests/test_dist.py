@@ -74,3 +74,86 @@ def test_gather_tiles_world2():
     for p in procs:
         p.join(timeout=60)
     assert res == {0: True, 1: True}
+
+
+def _fold_worker(rank, world, port, q):
+    """Each rank holds its partial histogram (m slots of ciphertexts, tile-major CPU layout);
+    the shards are all-gathered (gather_tiles) and every rank folds slot j over the ranks with
+    Ciphertext::add (the oracle's; bench.py does the same on the device with k_add27)."""
+    import json
+    import random
+
+    from oracle import paillier_oracle as O
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        here = os.path.dirname(os.path.abspath(__file__))
+        fx = json.load(open(os.path.join(here, "golden", "paillier_1024.json")))
+        osk, opk = O.keypair_from_primes(int(fx["p"], 16), int(fx["q"], 16))
+        m, L = 70, 64  # 70 slots: a partial last tile per rank
+        rng = random.Random(1000 + rank)
+        part = []
+        for j in range(m):  # signed ciphertexts, mixed exponents, a literal 1 now and then
+            c = rng.randrange(2, opk.ns)
+            part.append(O.ct_zero() if rng.random() < 0.1 else
+                        O.Ciphertext(-c if rng.random() < 0.4 else c, rng.choice([0, -1, -13, -14])))
+        nt = (m + WAVE - 1) // WAVE
+        C = torch.zeros((nt, L, WAVE), dtype=torch.int32)
+        sign = torch.zeros(nt * WAVE, dtype=torch.uint8)
+        exp = torch.zeros(nt * WAVE, dtype=torch.int32)
+        for k, ct in enumerate(part):
+            canon = ct.c + opk.ns if ct.c < 0 else ct.c
+            words = [(canon >> (32 * w)) & 0xFFFFFFFF for w in range(L)]
+            C[k // WAVE, :, k % WAVE] = torch.tensor(words, dtype=torch.int64).to(torch.int32)
+            sign[k] = 1 if ct.c < 0 else 0
+            exp[k] = ct.exp
+        Cg, sg, eg, total = gather_tiles(C, sign, exp, m)
+        assert total == world * m
+
+        def elem(g):
+            words = Cg[g // WAVE, :, g % WAVE].to(torch.int64) & 0xFFFFFFFF
+            v = sum(int(w) << (32 * i) for i, w in enumerate(words.tolist()))
+            return O.Ciphertext(v - opk.ns if (int(sg[g]) and v) else v, int(eg[g]))
+
+        folded = []
+        for j in range(m):
+            acc = elem(j)
+            for r in range(1, world):
+                acc = O.ct_add(opk, acc, elem(r * m + j))
+            folded.append((acc.c, acc.exp))
+        # every rank's partials, rebuilt from the same seeds, folded in a different order
+        want = []
+        parts = []
+        for r in range(world):
+            rr = random.Random(1000 + r)
+            pr = []
+            for j in range(m):
+                c = rr.randrange(2, opk.ns)
+                pr.append(O.ct_zero() if rr.random() < 0.1 else
+                          O.Ciphertext(-c if rr.random() < 0.4 else c, rr.choice([0, -1, -13, -14])))
+            parts.append(pr)
+        for j in range(m):
+            acc = O.ct_zero()
+            for r in reversed(range(world)):
+                acc = O.ct_add(opk, acc, parts[r][j])
+            want.append((acc.c, acc.exp))
+        q.put((rank, folded == want))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_cross_rank_ciphertext_fold_world2():
+    """SecureBoost's histogram across GPUs: per-rank partial folds,
+    all-gathered, then folded again with ct-add; bit-exact against a fold of the same
+    partials in another order, on world_size 2 over gloo."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fold_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: True, 1: True}

@@ -238,3 +238,51 @@ def test_random_op_chains_vs_oracle(k1024, seed):
     got = coder.decode_f64_vec(sk.decrypt_to_encoded(da)).cpu().tolist()
     want = [O.decode_f64(opk.n, d.significant, d.exp) for d in (O.fp_decrypt(osk, c) for c in oa)]
     assert [float(x) for x in got] == [float(x) for x in want]
+
+
+@pytest.mark.parametrize("bits", [512, 770, 1030, 1536])
+def test_other_key_sizes_bit_exact(bits):
+    """Even key sizes other than 1024 / 2048 (the reference takes any even size, paillier/
+    src/lib.rs:72-87; he_param.key_length is a job parameter) run the 1024- or 2048-bit
+    kernels with n zero-padded: encrypt (public and key-holder, injected r), ct-add with
+    exponent alignment, ct x pt with negative weights, neg and decrypt, bit-exact against
+    the oracle on a freshly generated key."""
+    import random
+    sk, pk, coder = P.keygen(bits)
+    assert pk.n.bit_length() == bits
+    osk, opk = O.keypair_from_primes(sk.p, sk.q)
+    rng = random.Random(bits)
+    xs = [rng.uniform(-9, 9) for _ in range(70)] + [0.0, -1e-300, 3e38]
+    ws = [rng.uniform(-2, 2) for _ in xs]
+    rs = [1 + rng.randrange(pk.n - 1) for _ in xs]
+    xd = torch.tensor(xs, dtype=torch.float64, device="cuda")
+    pv = coder.encode_f64_vec(xd)
+    pub = P.PK(pk.n)
+    c = pub.encrypt_encoded(pv, True, r=rs)
+    ck = pk.encrypt_encoded(pv, True, r=rs)  # key-holder CRT path
+    oc = [O.fp_encrypt(opk, O.encode_f64(opk.n, x), True, r) for x, r in zip(xs, rs)]
+    want = ([o.c for o in oc], [o.exp for o in oc])
+    assert c.to_signed_ints(pk.ns) == want and ck.to_signed_ints(pk.ns) == want
+    y = pub.encrypt_encoded(coder.encode_f64_vec(xd.flip(0) * 1e-3), True, r=rs[::-1])
+    oy = [O.fp_encrypt(opk, O.encode_f64(opk.n, x * 1e-3), True, r) for x, r in zip(xs[::-1], rs[::-1])]
+    s = c.add(pk, y)
+    assert s.to_signed_ints(pk.ns) == ([t.c for t in O.vec_add(opk, oc, oy)], [t.exp for t in O.vec_add(opk, oc, oy)])
+    m = c.mul(pk, coder.encode_f64_vec(torch.tensor(ws, dtype=torch.float64, device="cuda")))
+    om = [O.ct_mul(opk, a, O.encode_f64(opk.n, w)) for a, w in zip(oc, ws)]
+    assert m.to_signed_ints(pk.ns) == ([t.c for t in om], [t.exp for t in om])
+    ng = c.neg(pk)
+    assert ng.to_signed_ints(pk.ns)[0] == [O.ct_neg(opk, a).c for a in oc]
+    dec = sk.decrypt_to_encoded(s).to_ints()
+    od = [O.fp_decrypt(osk, t) for t in O.vec_add(opk, oc, oy)]
+    assert dec == ([d.significant for d in od], [d.exp for d in od])
+
+
+def test_unsupported_key_sizes_decline():
+    """Sizes this backend does not run fail at keygen with ValueError (FATE keeps its CPU
+    path for them); odd sizes fail like the reference's assert."""
+    from fate_amd import protocol as PR
+    assert PR.supports(2048) and PR.supports(1536) and not PR.supports(3072) and not PR.supports(1023)
+    with pytest.raises(ValueError):
+        PR.keygen(3072)
+    with pytest.raises(AssertionError):
+        P.keygen(1023)
