@@ -2,7 +2,8 @@
 //
 // Reference semantics: rust/fate_utils/crates/paillier/src/lib.rs (L0) and
 // rust/fate_utils/crates/fixedpoint_paillier/src/lib.rs (L1); SURVEY.md Appendix A.
-// The modexp kernels (kernels27.h) spread an element over TPI adjacent lanes (27-bit limbs);
+// The modexp kernels (kernels27.h) spread an element over TPI adjacent lanes (27-bit limbs at
+// TPI 4, 28-bit below: mont27_dev.h);
 // the codec, CRT-tail, permutation and wire kernels take one element per lane.  All run
 // grid-stride loops over 64-element tiles; see DESIGN.md for layouts and rooflines.
 #include <hip/hip_runtime.h>
@@ -44,18 +45,19 @@ struct KeyArgs {
   const u32* pinvqR;   // p^{-1} mod q, times R_q mod q
   u32 p2_n0inv, p_n0inv, q2_n0inv, q_n0inv;
   int pm1_bits, qm1_bits;
-  // reduced-radix engine (kernels27.h): 27-bit limbs, R = 2^(27 NL)
+  // reduced-radix engine (kernels27.h): LB-bit limbs (27 for n^2 of 2048-bit keys, 28 for
+  // every other modulus), R = 2^(LB NL); the _27 suffix names the engine, not the radix
   const u32* N2_27; const u32* N2R1_27; const u32* N2R2_27;  // n^2, R mod n^2, R^2 mod n^2 [NL2]
   const u32* P2_27; const u32* P2R1_27; const u32* P2R2_27;  // p^2 ...                      [NLh]
   const u32* Q2_27; const u32* Q2R1_27; const u32* Q2R2_27;
-  u32 n2_np27, p2_np27, q2_np27;                             // -N^{-1} mod 2^27
+  u32 n2_np27, p2_np27, q2_np27;                             // -N^{-1} mod 2^LB
   const u32* Nn_27; const u32* NnR1_27; const u32* NnR2_27;  // n, R mod n, R^2 mod n    [NLh]
-  u32 nn_np27, nn_inv27;                                     // -n^{-1}, n^{-1} mod 2^27
+  u32 nn_np27, nn_inv27;                                     // -n^{-1}, n^{-1} mod 2^LB
   // key-holder (CRT) encryption, valid iff has_sk: r^n mod s^2 = r^(n mod s(s-1)) mod s^2,
   // recombined as x_p Kp + x_q Kq mod n^2 (Kp = q^2 (q^-2 mod p^2), Kq = p^2 (p^-2 mod q^2))
   const u32* ep; const u32* eq;          // n mod p(p-1), n mod q(q-1)           [L1]
   int ep_bits, eq_bits;
-  const u32* KpR_27; const u32* KqR_27;  // Kp R, Kq R mod n^2 (27-bit, R = 2^(27 NL2)) [NL2]
+  const u32* KpR_27; const u32* KqR_27;  // Kp R, Kq R mod n^2 (R = 2^(LB NL2))         [NL2]
   const u32* FR_27;                      // R^k mod n^2, k = 0..kFoldMax               [kFoldMax+1][NL2]
 };
 
@@ -515,15 +517,15 @@ struct DevGuard {
 
 Limbs from_words(const uint32_t* w, size_t n) { return hbn::norm(Limbs(w, w + n)); }
 
-// little-endian 32-bit words -> nl 27-bit limbs
-Limbs to27(const Limbs& v, int nl) {
+// little-endian 32-bit words -> nl limbs of lb bits (the engine radix of the modulus)
+Limbs to_radix(const Limbs& v, int nl, int lb) {
   Limbs o((size_t)nl, 0u);
   for (int i = 0; i < nl; ++i) {
-    const size_t bit = (size_t)27 * i, w = bit >> 5;
+    const size_t bit = (size_t)lb * i, w = bit >> 5;
     const unsigned off = (unsigned)(bit & 31);
     u64 x = w < v.size() ? v[w] : 0u;
     if (w + 1 < v.size()) x |= (u64)v[w + 1] << 32;
-    o[(size_t)i] = (u32)(x >> off) & ((1u << 27) - 1u);
+    o[(size_t)i] = (u32)(x >> off) & ((1u << lb) - 1u);
   }
   return o;
 }
@@ -583,12 +585,12 @@ template <int L>
 fphe_status launch_encrypt27(fphe_ctx* c, const uint32_t* P, uint32_t lp, const uint8_t* neg, size_t count, int obf,
                              const uint32_t* r, const uint32_t key[8], uint64_t nonce, uint32_t* C, uint8_t* sign,
                              hipStream_t s) {
-  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = r27::LL * TPI, LDSW = NL > L ? NL : L, L1 = L / 2;
-  auto kern = k_encrypt27<L, kWinSlide>;
+  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = rad_ll(TPI) * TPI, LDSW = NL > L ? NL : L, L1 = L / 2;
+  auto kern = KS<TPI>::template encrypt<L, kWinSlide>();
   const size_t lds = (size_t)kWavesPerBlock * LDSW * E * 4;
   set_lds(kern, lds);
   const unsigned grid = occ_grid(c, kern, lds, (count + E - 1) / E, "encrypt27");
-  const size_t tbytes = (size_t)grid * kWavesPerBlock * kTabEntries<kWinSlide> * r27::LL * FPHE_WAVE * 4;
+  const size_t tbytes = (size_t)grid * kWavesPerBlock * kTabEntries<kWinSlide> * rad_ll(TPI) * FPHE_WAVE * 4;
   const size_t rbytes = (size_t)ntiles_of(count) * L1 * FPHE_WAVE * 4;
   const bool draw = obf && !r;
   if (ensure_scratch(c, tbytes + (draw ? rbytes : 0), s) != FPHE_OK) return FPHE_ERR_HIP;
@@ -608,12 +610,12 @@ fphe_status launch_encrypt27(fphe_ctx* c, const uint32_t* P, uint32_t lp, const 
 
 template <int L>
 fphe_status launch_decrypt27(fphe_ctx* c, const uint32_t* C, size_t count, uint32_t* P, hipStream_t s) {
-  constexpr int TPI = L / 64, E = FPHE_WAVE / TPI, NL = r27::LL * TPI, LH = L / 2, LQ = L / 4;
-  auto kern = k_pow_half27<L, kWinSlide, false>;
+  constexpr int TPI = L / 64, E = FPHE_WAVE / TPI, NL = rad_ll(TPI) * TPI, LH = L / 2, LQ = L / 4;
+  auto kern = KS<TPI>::template pow_half<L, kWinSlide, false>();
   const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
   set_lds(kern, lds);
   const unsigned grid = occ_grid(c, kern, lds, (count + E - 1) / E, "decrypt_pow27");
-  const size_t tbytes = (size_t)grid * kWavesPerBlock * kTabEntries<kWinSlide> * r27::LL * FPHE_WAVE * 4;
+  const size_t tbytes = (size_t)grid * kWavesPerBlock * kTabEntries<kWinSlide> * rad_ll(TPI) * FPHE_WAVE * 4;
   const size_t ybytes = (size_t)ntiles_of(count) * 2 * LH * FPHE_WAVE * 4;
   if (ensure_scratch(c, tbytes + ybytes, s) != FPHE_OK) return FPHE_ERR_HIP;
   u32* Y = c->scratch + tbytes / 4;
@@ -632,13 +634,13 @@ template <int L>
 fphe_status launch_encrypt_crt27(fphe_ctx* c, const uint32_t* P, uint32_t lp, const uint8_t* neg, size_t count,
                                  const uint32_t* r, const uint32_t key[8], uint64_t nonce, uint32_t* C,
                                  uint8_t* sign, hipStream_t s) {
-  constexpr int TPIh = L / 64, Eh = FPHE_WAVE / TPIh, NLh = r27::LL * TPIh, L1 = L / 2;
-  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = r27::LL * TPI, LDSW = NL > L + 2 ? NL : L + 2;
-  auto k1 = k_pow_half27<L, kWinSlide, true>;
+  constexpr int TPIh = L / 64, Eh = FPHE_WAVE / TPIh, NLh = rad_ll(TPIh) * TPIh, L1 = L / 2;
+  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = rad_ll(TPI) * TPI, LDSW = NL > L + 2 ? NL : L + 2;
+  auto k1 = KS<TPIh>::template pow_half<L, kWinSlide, true>();
   const size_t lds1 = (size_t)kWavesPerBlock * NLh * Eh * 4;
   set_lds(k1, lds1);
   const unsigned g1 = occ_grid(c, k1, lds1, (count + Eh - 1) / Eh, "pow_half27<enc>");
-  const size_t tbytes = (size_t)g1 * kWavesPerBlock * kTabEntries<kWinSlide> * r27::LL * FPHE_WAVE * 4;
+  const size_t tbytes = (size_t)g1 * kWavesPerBlock * kTabEntries<kWinSlide> * rad_ll(TPIh) * FPHE_WAVE * 4;
   const size_t ybytes = (size_t)ntiles_of(count) * 2 * L1 * FPHE_WAVE * 4;
   const size_t rbytes = (size_t)ntiles_of(count) * L1 * FPHE_WAVE * 4;
   if (ensure_scratch(c, tbytes + ybytes + (r ? 0 : rbytes), s) != FPHE_OK) return FPHE_ERR_HIP;
@@ -653,7 +655,7 @@ fphe_status launch_encrypt_crt27(fphe_ctx* c, const uint32_t* P, uint32_t lp, co
     rbuf = rdev;
   }
   hipLaunchKernelGGL(k1, dim3(g1), dim3(kBlock), lds1, s, c->K, rbuf, count, Y, c->scratch, (u32)NLh);
-  auto k2 = k_encrypt_crt27<L>;
+  auto k2 = KS<TPI>::template encrypt_crt<L>();
   const size_t lds2 = (size_t)kWavesPerBlock * LDSW * E * 4;
   set_lds(k2, lds2);
   const unsigned g2 = occ_grid(c, k2, lds2, (count + E - 1) / E, "encrypt_crt27");
@@ -665,8 +667,8 @@ template <int L>
 fphe_status launch_fold27(fphe_ctx* c, const uint32_t* Src, const uint8_t* ssign, const int32_t* sexp,
                           const int64_t* ord, const int64_t* cstart, const int32_t* clen, size_t nchunks,
                           uint32_t* Co, uint8_t* so, int32_t* eo, hipStream_t s) {
-  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = r27::LL * TPI;
-  auto kern = k_fold27<L>;
+  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = rad_ll(TPI) * TPI;
+  auto kern = KS<TPI>::template fold<L>();
   const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
   set_lds(kern, lds);
   const unsigned grid = occ_grid(c, kern, lds, (nchunks + E - 1) / E, "fold27");
@@ -685,8 +687,8 @@ template <int L>
 fphe_status launch_add27(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, const int32_t* ea, const uint32_t* Cb,
                          const uint8_t* sb, const int32_t* eb, int bstride, size_t count, const int32_t* ord,
                          uint32_t* Co, uint8_t* so, int32_t* eo, hipStream_t s) {
-  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = r27::LL * TPI;
-  auto kern = k_add27<L>;
+  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = rad_ll(TPI) * TPI;
+  auto kern = KS<TPI>::template add<L>();
   const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
   set_lds(kern, lds);
   const size_t cmax = add_max_count(L);
@@ -705,8 +707,8 @@ fphe_status launch_add27(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, con
 template <int L>
 fphe_status launch_sqmul27(fphe_ctx* c, const uint32_t* Ca, const uint32_t* Cb, const uint8_t* sb, int nsq,
                            size_t count, uint32_t* Co, uint8_t* so, hipStream_t s) {
-  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = r27::LL * TPI;
-  auto kern = k_sqmul27<L>;
+  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = rad_ll(TPI) * TPI;
+  auto kern = KS<TPI>::template sqmul<L>();
   const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
   set_lds(kern, lds);
   const unsigned grid = occ_grid(c, kern, lds, (count + E - 1) / E, "sqmul27");
@@ -718,15 +720,15 @@ fphe_status launch_sqmul27(fphe_ctx* c, const uint32_t* Ca, const uint32_t* Cb, 
 template <int L>
 void launch_inv27(fphe_ctx* c, const uint32_t* Ca, size_t count, const uint8_t* need, uint32_t* Co,
                   int32_t* err, u32* X0, hipStream_t s) {
-  constexpr int TPIh = L / 64, Eh = FPHE_WAVE / TPIh, NLh = r27::LL * TPIh, L1 = L / 2;
-  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = r27::LL * TPI;
-  auto k1 = k_inv_n27<L>;
+  constexpr int TPIh = L / 64, Eh = FPHE_WAVE / TPIh, NLh = rad_ll(TPIh) * TPIh, L1 = L / 2;
+  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = rad_ll(TPI) * TPI;
+  auto k1 = KS<TPIh>::template inv_n<L>();
   const size_t lds1 = (size_t)kWavesPerBlock * NLh * Eh * 4;
   set_lds(k1, lds1);
   const unsigned g1 = occ_grid(c, k1, lds1, (count + Eh - 1) / Eh, "inv_n27");
   (void)L1;
   hipLaunchKernelGGL(k1, dim3(g1), dim3(kBlock), lds1, s, c->K, Ca, count, need, X0, err, (u32)NLh);
-  auto k2 = k_inv_lift27<L>;
+  auto k2 = KS<TPI>::template inv_lift<L>();
   const size_t lds2 = (size_t)kWavesPerBlock * NL * E * 4;
   set_lds(k2, lds2);
   const unsigned g2 = occ_grid(c, k2, lds2, (count + E - 1) / E, "inv_lift27");
@@ -741,7 +743,7 @@ template <int L>
 size_t binv_scratch_bytes(size_t count) {
   constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, PER = FPHE_WAVE / E, KB = 4 * PER;
   const size_t nwt = (ntiles_of(count) + 3) / 4, ntot = nwt * E;
-  return nwt * KB * r27::LL * FPHE_WAVE * 4 + 2 * (size_t)ntiles_of(ntot) * L * FPHE_WAVE * 4 +
+  return nwt * KB * rad_ll(TPI) * FPHE_WAVE * 4 + 2 * (size_t)ntiles_of(ntot) * L * FPHE_WAVE * 4 +
          (size_t)ntiles_of(ntot) * (L / 2) * FPHE_WAVE * 4;
 }
 
@@ -754,21 +756,21 @@ size_t binv_min() {
 template <int L>
 void launch_binv27(fphe_ctx* c, const uint32_t* Ca, size_t count, const uint8_t* need, uint32_t* Co, int32_t* err,
                    u32* W, hipStream_t s) {
-  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = r27::LL * TPI, PER = FPHE_WAVE / E, KB = 4 * PER;
+  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = rad_ll(TPI) * TPI, PER = FPHE_WAVE / E, KB = 4 * PER;
   const size_t nwt = (ntiles_of(count) + 3) / 4, ntot = nwt * E;
-  const size_t tab_words = nwt * KB * r27::LL * FPHE_WAVE;
+  const size_t tab_words = nwt * KB * rad_ll(TPI) * FPHE_WAVE;
   const size_t tot_words = (size_t)ntiles_of(ntot) * L * FPHE_WAVE;
   u32* Tab = W;
   u32* Tot = Tab + tab_words;
   u32* Inv = Tot + tot_words;
   u32* X0 = Inv + tot_words;
   const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
-  auto k1 = k_binv_pre27<L>;
+  auto k1 = KS<TPI>::template binv_pre<L>();
   set_lds(k1, lds);
   const unsigned g1 = occ_grid(c, k1, lds, nwt, "binv_pre27");
   hipLaunchKernelGGL(k1, dim3(g1), dim3(kBlock), lds, s, c->K, Ca, count, need, Tab, Tot, (u32)NL);
   launch_inv27<L>(c, Tot, ntot, nullptr, Inv, err, X0, s);
-  auto k2 = k_binv_post27<L>;
+  auto k2 = KS<TPI>::template binv_post<L>();
   set_lds(k2, lds);
   const unsigned g2 = occ_grid(c, k2, lds, nwt, "binv_post27");
   hipLaunchKernelGGL(k2, dim3(g2), dim3(kBlock), lds, s, c->K, Ca, count, need, Tab, Inv, Co, (u32)NL);
@@ -779,14 +781,14 @@ fphe_status launch_mul27(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, con
                          uint32_t lp, const uint8_t* pneg, const int32_t* pexp, int pstride, size_t count,
                          uint32_t* Co, uint8_t* so, int32_t* eo, int32_t* err, hipStream_t s) {
   (void)sa;  // powm results are canonical whatever the base's sign (lib.rs:334-349)
-  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = r27::LL * TPI, L1 = L / 2;
-  auto kern = k_mul27<L, kWinMul>;
+  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = rad_ll(TPI) * TPI, L1 = L / 2;
+  auto kern = KS<TPI>::template mul<L, kWinMul>();
   const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
   set_lds(kern, lds);
   const unsigned grid = occ_grid(c, kern, lds, (count + E - 1) / E, "mul27");
   // scratch: [window tables][need T*64 B][ebits T*64 i32][E T*L1*64 w][Cinv T*L*64 w][X0 T*L1*64 w]
   const size_t nt = ntiles_of(count);
-  const size_t tbytes = (size_t)grid * kWavesPerBlock * (1u << kWinMul) * r27::LL * FPHE_WAVE * 4;
+  const size_t tbytes = (size_t)grid * kWavesPerBlock * (1u << kWinMul) * rad_ll(TPI) * FPHE_WAVE * 4;
   const size_t o_need = tbytes, o_eb = o_need + nt * FPHE_WAVE, o_E = o_eb + nt * FPHE_WAVE * 4;
   const bool batch = count >= binv_min();
   const size_t o_inv = o_E + nt * L1 * FPHE_WAVE * 4, o_x0 = o_inv + nt * L * FPHE_WAVE * 4;
@@ -1075,24 +1077,32 @@ fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, 
     max_int = hbn::norm(max_int);
     const size_t o_max = put(max_int, L1);
     const size_t o_nmm = put(hbn::sub(n, max_int), L1);
-    const int NL2 = 38 * (L2 / 32), NLh = 38 * (L2 / 64);
-    const size_t o_N2_27 = put(to27(N2, NL2), NL2);
-    const size_t o_N2R1_27 = put(to27(hbn::pow2_mod((size_t)27 * NL2, N2), NL2), NL2);
-    const size_t o_N2R2_27 = put(to27(hbn::pow2_mod((size_t)54 * NL2, N2), NL2), NL2);
+    // engine limbs: n^2 at TPI2 = L2/32 lanes, n / p^2 / q^2 at TPIh = L2/64, each in the
+    // radix of its engine (mont27_dev.h: 27 bits at TPI 4, 28 below); R = 2^(LB NL)
+    const int TPI2 = L2 / 32, TPIh = L2 / 64;
+    const int LB2 = rad_lb(TPI2), LBh = rad_lb(TPIh);
+    const int NL2 = rad_ll(TPI2) * TPI2, NLh = rad_ll(TPIh) * TPIh;
+    auto to27 = [](const Limbs& v, int nl, int lb) { return to_radix(v, nl, lb); };
+    const size_t o_N2_27 = put(to27(N2, NL2, LB2), NL2);
+    const size_t o_N2R1_27 = put(to27(hbn::pow2_mod((size_t)LB2 * NL2, N2), NL2, LB2), NL2);
+    const size_t o_N2R2_27 = put(to27(hbn::pow2_mod((size_t)2 * LB2 * NL2, N2), NL2, LB2), NL2);
     // R^k mod n^2, k = 0..kFoldMax (27-bit limbs): the k_fold27 fix-up factors
     size_t o_FR = 0;
     {
-      const Limbs R27 = hbn::pow2_mod((size_t)27 * NL2, N2);
-      Limbs x{1};
+      // rows of exactly NL2 limbs, back to back (k_fold27 indexes row k at k * NL): one put,
+      // since put() pads each section to 16 bytes and NL2 = 74 is not a multiple of 4
+      const Limbs R27 = hbn::pow2_mod((size_t)LB2 * NL2, N2);
+      Limbs x{1}, rows;
       for (int k = 0; k <= kFoldMax; ++k) {
-        const size_t o = put(to27(x, NL2), NL2);
-        if (k == 0) o_FR = o;
+        const Limbs r = to27(x, NL2, LB2);
+        rows.insert(rows.end(), r.begin(), r.end());
         x = hbn::mod(hbn::mul(x, R27), N2);
       }
+      o_FR = put(rows, rows.size());
     }
-    const size_t o_Nn_27 = put(to27(n, NLh), NLh);
-    const size_t o_NnR1_27 = put(to27(hbn::pow2_mod((size_t)27 * NLh, n), NLh), NLh);
-    const size_t o_NnR2_27 = put(to27(hbn::pow2_mod((size_t)54 * NLh, n), NLh), NLh);
+    const size_t o_Nn_27 = put(to27(n, NLh, LBh), NLh);
+    const size_t o_NnR1_27 = put(to27(hbn::pow2_mod((size_t)LBh * NLh, n), NLh, LBh), NLh);
+    const size_t o_NnR2_27 = put(to27(hbn::pow2_mod((size_t)2 * LBh * NLh, n), NLh, LBh), NLh);
     size_t o_P2_27 = 0, o_P2R1_27 = 0, o_P2R2_27 = 0, o_Q2_27 = 0, o_Q2R1_27 = 0, o_Q2R2_27 = 0;
     size_t o_P2 = 0, o_P2R3 = 0, o_pm1 = 0, o_p = 0, o_pinv2 = 0, o_hpR = 0;
     size_t o_Q2 = 0, o_Q2R3 = 0, o_qm1 = 0, o_q = 0, o_qinv2 = 0, o_hqR = 0, o_pinvqR = 0;
@@ -1129,12 +1139,12 @@ fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, 
       o_qinv2 = put(hbn::inv_pow2(q, LQ), LQ);
       o_hqR = put(hbn::mod(hbn::mul(hq, hbn::pow2_mod((size_t)32 * LQ, q)), q), LQ);
       o_pinvqR = put(hbn::mod(hbn::mul(pinvq, hbn::pow2_mod((size_t)32 * LQ, q)), q), LQ);
-      o_P2_27 = put(to27(P2, NLh), NLh);
-      o_P2R1_27 = put(to27(hbn::pow2_mod((size_t)27 * NLh, P2), NLh), NLh);
-      o_P2R2_27 = put(to27(hbn::pow2_mod((size_t)54 * NLh, P2), NLh), NLh);
-      o_Q2_27 = put(to27(Q2, NLh), NLh);
-      o_Q2R1_27 = put(to27(hbn::pow2_mod((size_t)27 * NLh, Q2), NLh), NLh);
-      o_Q2R2_27 = put(to27(hbn::pow2_mod((size_t)54 * NLh, Q2), NLh), NLh);
+      o_P2_27 = put(to27(P2, NLh, LBh), NLh);
+      o_P2R1_27 = put(to27(hbn::pow2_mod((size_t)LBh * NLh, P2), NLh, LBh), NLh);
+      o_P2R2_27 = put(to27(hbn::pow2_mod((size_t)2 * LBh * NLh, P2), NLh, LBh), NLh);
+      o_Q2_27 = put(to27(Q2, NLh, LBh), NLh);
+      o_Q2R1_27 = put(to27(hbn::pow2_mod((size_t)LBh * NLh, Q2), NLh, LBh), NLh);
+      o_Q2R2_27 = put(to27(hbn::pow2_mod((size_t)2 * LBh * NLh, Q2), NLh, LBh), NLh);
       p2n0 = hbn::neg_inv32(P2[0]); pn0 = hbn::neg_inv32(p[0]);
       q2n0 = hbn::neg_inv32(Q2[0]); qn0 = hbn::neg_inv32(q[0]);
       pm1b = (int)hbn::bitlen(pm1); qm1b = (int)hbn::bitlen(qm1);
@@ -1143,11 +1153,11 @@ fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, 
       o_ep = put(ep, L1);
       o_eq = put(eq, L1);
       epb = (int)hbn::bitlen(ep); eqb = (int)hbn::bitlen(eq);
-      const Limbs R27 = hbn::pow2_mod((size_t)27 * NL2, N2);
+      const Limbs R27 = hbn::pow2_mod((size_t)LB2 * NL2, N2);
       const Limbs Kp = hbn::mul(Q2, hbn::inv_mod(hbn::mod(Q2, P2), P2));  // < n^2
       const Limbs Kq = hbn::mul(P2, hbn::inv_mod(hbn::mod(P2, Q2), Q2));
-      o_KpR = put(to27(hbn::mod(hbn::mul(Kp, R27), N2), NL2), NL2);
-      o_KqR = put(to27(hbn::mod(hbn::mul(Kq, R27), N2), NL2), NL2);
+      o_KpR = put(to27(hbn::mod(hbn::mul(Kp, R27), N2), NL2, LB2), NL2);
+      o_KqR = put(to27(hbn::mod(hbn::mul(Kq, R27), N2), NL2, LB2), NL2);
     }
     auto* c = new fphe_ctx();
     c->device = device; c->key_bits = key_bits; c->L1 = L1; c->L2 = L2; c->LQ = LQ; c->has_sk = has_sk;
@@ -1166,11 +1176,11 @@ fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, 
     K.n2_n0inv = hbn::neg_inv32(N2[0]);
     K.nbits = (int)key_bits;
     K.N2_27 = b + o_N2_27; K.N2R1_27 = b + o_N2R1_27; K.N2R2_27 = b + o_N2R2_27;
-    K.n2_np27 = K.n2_n0inv & ((1u << 27) - 1u);
+    K.n2_np27 = K.n2_n0inv & ((1u << LB2) - 1u);
     K.FR_27 = b + o_FR;
     K.Nn_27 = b + o_Nn_27; K.NnR1_27 = b + o_NnR1_27; K.NnR2_27 = b + o_NnR2_27;
-    K.nn_np27 = hbn::neg_inv32(n[0]) & ((1u << 27) - 1u);
-    K.nn_inv27 = (0u - hbn::neg_inv32(n[0])) & ((1u << 27) - 1u);
+    K.nn_np27 = hbn::neg_inv32(n[0]) & ((1u << LBh) - 1u);
+    K.nn_inv27 = (0u - hbn::neg_inv32(n[0])) & ((1u << LBh) - 1u);
     if (has_sk) {
       K.P2 = b + o_P2; K.P2_R3 = b + o_P2R3; K.pm1 = b + o_pm1; K.p = b + o_p; K.pinv2 = b + o_pinv2; K.hpR = b + o_hpR;
       K.Q2 = b + o_Q2; K.Q2_R3 = b + o_Q2R3; K.qm1 = b + o_qm1; K.q = b + o_q; K.qinv2 = b + o_qinv2; K.hqR = b + o_hqR;
@@ -1179,7 +1189,7 @@ fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, 
       K.pm1_bits = pm1b; K.qm1_bits = qm1b;
       K.P2_27 = b + o_P2_27; K.P2R1_27 = b + o_P2R1_27; K.P2R2_27 = b + o_P2R2_27;
       K.Q2_27 = b + o_Q2_27; K.Q2R1_27 = b + o_Q2R1_27; K.Q2R2_27 = b + o_Q2R2_27;
-      K.p2_np27 = p2n0 & ((1u << 27) - 1u); K.q2_np27 = q2n0 & ((1u << 27) - 1u);
+      K.p2_np27 = p2n0 & ((1u << LBh) - 1u); K.q2_np27 = q2n0 & ((1u << LBh) - 1u);
       K.ep = b + o_ep; K.eq = b + o_eq; K.ep_bits = epb; K.eq_bits = eqb;
       K.KpR_27 = b + o_KpR; K.KqR_27 = b + o_KqR;
     }

@@ -54,11 +54,43 @@ def test_sliding_window_schedule_matches_walk(seed):
 
 
 def test_generated_asm_headers_in_sync():
-    """fate_amd/csrc/mont27_*_gen.h are exactly what tools/gen_mont27_asm.py writes."""
+    """fate_amd/csrc/mont_gen_ll{38,37}.h are exactly what tools/gen_mont27_asm.py writes."""
     with tempfile.TemporaryDirectory() as d:
         shutil.copytree(os.path.join(ROOT, "tools"), os.path.join(d, "tools"))
         os.makedirs(os.path.join(d, "fate_amd", "csrc"))
         subprocess.run([sys.executable, os.path.join(d, "tools", "gen_mont27_asm.py")], check=True)
-        for name in ("mont27_asm_gen.h", "mont27_sq_gen.h", "mont27_fused_gen.h"):
+        for name in ("mont_gen_ll38.h", "mont_gen_ll37.h"):
             assert filecmp.cmp(os.path.join(d, "fate_amd", "csrc", name),
                                os.path.join(ROOT, "fate_amd", "csrc", name), shallow=False), name
+
+
+@pytest.mark.parametrize("tpi,ll", [(4, 38), (2, 38), (1, 38), (2, 37), (1, 37)])
+def test_squaring_window_adds_every_limb_pair_once(tpi, ll):
+    """The half-product squaring (mont_engine.inc mont_sqr, rows from the generator's
+    sq_window) adds each off-diagonal limb pair exactly twice (once, doubled) and each
+    diagonal term once, for the 27 x 38 (TPI 4) and 28 x 37 (TPI 1, 2) engines.  Multiplier
+    rules as the kernel's bit-field masks: bf = 2a (q > s), a (q == s), 0 (q < s); bl (even
+    LL only) = 2a if q < s or (q == s and a < LL/2), else 0; bm = 2a."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("gen27", os.path.join(ROOT, "tools", "gen_mont27_asm.py"))
+    gen = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gen)
+    from collections import Counter
+    cov = Counter()
+    nl = tpi * ll
+    for s in range(tpi):
+        for a in range(ll):
+            i = ll * s + a
+            for q in range(tpi):
+                for k, mul in gen.sq_window(ll, a):
+                    g = ll * q + k
+                    if mul == "bf":
+                        f = 2 if q > s else (1 if q == s else 0)
+                    elif mul == "bl":
+                        f = 2 if (q < s or (q == s and a < ll // 2)) else 0
+                    else:
+                        f = 2
+                    if f:
+                        cov[(min(i, g), max(i, g))] += f
+    assert set(cov) == {(x, y) for x in range(nl) for y in range(x, nl)}
+    assert all(c == (1 if x == y else 2) for (x, y), c in cov.items())

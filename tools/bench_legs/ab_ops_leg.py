@@ -1,0 +1,45 @@
+"""Same-box A/B leg (tools/gpu_job_ab_ops2.sh): times one warm launch each of encrypt
+(2^18, public key), decrypt (2^18), Hetero-LR-shaped ct-add (2^20) and ct x pt (2^18) at
+2048 bits, and encrypt / decrypt at 1024 bits, for the library FPHE_LIB_PATH names."""
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+from fate_amd import paillier as P  # noqa: E402
+
+dev = torch.device("cuda", 0)
+
+
+def t(f, *args):
+    f(*args)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    f(*args)
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0
+
+
+out = {}
+fx = json.load(open(os.path.join(ROOT, "tests", "golden", "paillier_2048.json")))
+sk, pk, coder = P.keypair_from_primes(int(fx["p"], 16), int(fx["q"], 16))
+g = torch.Generator().manual_seed(7)
+x = (torch.randn(1 << 20, generator=g) * 4).to(dev)
+a = pk.encrypt_encoded(coder.encode_f32_vec(x), True)
+b = pk.encrypt_encoded(coder.encode_f32_vec(torch.flip(x, [0]) * 0.25), True)
+q = coder.encode_f32_vec(x[: 1 << 18])
+out["enc2048_ms"] = round(1e3 * t(lambda: pk.encrypt_encoded(q, True)), 2)
+a18 = a.slice(0, 1 << 18)
+out["dec2048_ms"] = round(1e3 * t(lambda: sk.decrypt_to_encoded(a18)), 2)
+out["add2048_ms"] = round(1e3 * t(lambda: a.add(pk, b)), 3)
+out["mul2048_ms"] = round(1e3 * t(lambda: a18.mul(pk, q)), 2)
+sk1, pk1, coder1 = P.keygen(1024)
+q1 = coder1.encode_f32_vec(x[: 1 << 18])
+c1 = pk1.encrypt_encoded(q1, True)
+out["enc1024_ms"] = round(1e3 * t(lambda: pk1.encrypt_encoded(q1, True)), 2)
+out["dec1024_ms"] = round(1e3 * t(lambda: sk1.decrypt_to_encoded(c1)), 2)
+print(json.dumps(out))

@@ -1,141 +1,162 @@
-"""Generate fate_amd/csrc/mont27_asm_gen.h: one CIOS row of the 27-bit engine as asm blocks,
-each MAC one v_mad_u64_u32 on a 64-bit lazy accumulator.  Emitting a whole row per asm
+"""Generate fate_amd/csrc/mont_gen_ll38.h (27-bit limbs, 38 per lane) and mont_gen_ll37.h
+(28-bit limbs, 37 per lane): the CIOS rows of the reduced-radix engine as asm blocks, each
+MAC one v_mad_u64_u32 on a 64-bit lazy accumulator.  Emitting a whole row per asm
 statement keeps the compiler's conservative inline-asm hazard padding (s_nop) at block
 boundaries instead of between every MAC.
 
-Blocks:
-  R27_ASM_OPROW      t_j += a_j * b                         (LL MACs, general product)
-  R27_ASM_REDROW     x = m n_0 + t_0 ; t_{j-1} = m n_j + t_j (LL MACs, reduction + shift)
-  R27_ASM_SQROW_<a>  the squaring row for lane-slice row index a (0 <= a < LL): 20 MACs on
-                     the circular window of positions (a + s) mod LL, s = 0..19, with
-                     multiplier bf at s = 0, bm at s = 1..18, bl at s = 19.  See
-                     mont27_dev.h mont_sqr for why this covers each limb pair exactly once.
+Each file has sections, picked by RG_SECTION before each #include (mont_engine.inc):
+  1  macros   RG_OPROW      t_j += a_j * b                          (LL MACs, general product)
+              RG_REDROW     x = m n_0 + t_0 ; t_{j-1} = m n_j + t_j  (LL MACs, reduction + shift)
+              RG_SQROW_<a>  the squaring row for lane-slice row index a (0 <= a < LL): MACs on
+                            the circular window of positions (a + s) mod LL, s = 0..W-1 with
+                            W = LL/2 + 1, multiplier bf at s = 0, bm inside, and for even LL
+                            bl at s = W-1 (odd LL needs no half-window column).  See
+                            mont_engine.inc mont_sqr for why this covers each limb pair once.
+              RGF_ROW / RGF_SQROW_<a>  fused rows (below)
+  2  dispatchers r27_sqrow<a>        (after the limb vector type)
+  3  dispatchers r27f_sqrow<TPI, a>, r27f_row<TPI>  (after Mod)
+  4  #undef of every macro of section 1, so the other radix can define them again
 """
 import os
 
-LL = 38
-WIN = LL // 2 + 1  # 20
-out = []
-out.append("// Generated by tools/gen_mont27_asm.py -- do not edit.")
-out.append("#pragma once")
-row = "".join(f'"v_mad_u64_u32 %[t{j}], vcc, %[a{j}], %[b], %[t{j}]\\n\\t" ' for j in range(LL))
-out.append(f"#define R27_ASM_OPROW {row}")
-red = '"v_mad_u64_u32 %[x], vcc, %[m], %[n0], %[t0]\\n\\t" '
-red += "".join(f'"v_mad_u64_u32 %[t{j-1}], vcc, %[m], %[n{j}], %[t{j}]\\n\\t" ' for j in range(1, LL))
-out.append(f"#define R27_ASM_REDROW {red}")
-for a in range(LL):
+HERE = os.path.dirname(__file__)
+
+
+def sq_window(LL, a):
+    """(lane-local position, multiplier) of squaring row a: positions (a + s) mod LL for
+    s < LL/2 + 1; bf at s = 0, bl at the last s when LL is even, bm otherwise."""
+    WIN = LL // 2 + 1
     pos = []
     for s in range(WIN):
         k = (a + s) % LL
-        mul = "bf" if s == 0 else ("bl" if s == WIN - 1 else "bm")
+        if s == 0:
+            mul = "bf"
+        elif s == WIN - 1 and LL % 2 == 0:
+            mul = "bl"
+        else:
+            mul = "bm"
         pos.append((k, mul))
     pos.sort()  # ascending position: t0 (read next by the m computation) is written first
-    body = "".join(f'"v_mad_u64_u32 %[t{k}], vcc, %[a{k}], %[{mul}], %[t{k}]\\n\\t" ' for k, mul in pos)
-    out.append(f"#define R27_ASM_SQROW_{a} {body}")
-out.append("#define R27_T_OPS(T) " + ", ".join(f'[t{j}] "+v"(T[{j}])' for j in range(LL)))
-out.append("#define R27_A_INS(A) " + ", ".join(f'[a{j}] "v"(A[{j}])' for j in range(LL)))
-out.append("#define R27_N_INS(N, C) " + ", ".join(f'[n{j}] C(N({j}))' for j in range(LL)))
-path = os.path.join(os.path.dirname(__file__), "..", "fate_amd", "csrc", "mont27_asm_gen.h")
-with open(path, "w") as f:
-    f.write("\n".join(out) + "\n")
-# dispatcher r27_sqrow<a>(T, A, bf, bm, bl): included inside namespace fphe::r27 after L27
-out = ["// Generated by tools/gen_mont27_asm.py -- do not edit.", "#pragma once"]
-out.append("template <int a> __device__ __forceinline__ void r27_sqrow(u64 (&T)[LL], const L27& A, u32 bf, u32 bm, u32 bl);")
-for a in range(LL):
-    out.append(f"template <> __device__ __forceinline__ void r27_sqrow<{a}>(u64 (&T)[LL], const L27& A, u32 bf, u32 bm, u32 bl) {{")
-    out.append(f'  asm volatile(R27_ASM_SQROW_{a} : R27_T_OPS(T) : R27_A_INS(A), [bf] "v"(bf), [bm] "v"(bm), [bl] "v"(bl) : "vcc", "memory");')
-    out.append("}")
-path = os.path.join(os.path.dirname(__file__), "..", "fate_amd", "csrc", "mont27_sq_gen.h")
-with open(path, "w") as f:
-    f.write("\n".join(out) + "\n")
-
-# ---- fused rows: operand MACs + m + reduction MACs + the X fix-up in ONE asm block -------
-# The accumulator limb 0 and 37 are pinned to v[2:3] / v[4:5] and the row's temporaries to
-# v6..v11, so the block can address their 32-bit halves (inline asm has no sub-register
-# syntax).  Order inside the block:
-#   t0's operand MAC (if the row has one) -> v_mul_lo (m = t0 n' mod 2^27, broadcast from the
-#   element's lane 0 by the DPP AND) issued under the remaining operand MACs, then the
-#   reduction MACs with X = m n0 + t0 first; X >> 27 is added to the new t0 in the shadow of
-#   the later MACs, and X mod 2^27 moves to the lane below's top limb with a DPP AND.
-# Hazards honoured by construction: >= 2 VALU instructions between the VALU write of v10 and
-# its DPP read; X (v6) is written 36 instructions before its DPP read.
-# BC is the DPP broadcast control string for TPI (quad_perm:[0,0,0,0] / [0,0,2,2]).
-def treg(k):
-    return "v[2:3]" if k == 0 else ("v[4:5]" if k == LL - 1 else f"%[t{k}]")
+    return pos
 
 
-def fused(pos, spread):
-    """spread = (MACs between v_mul_lo and its DPP use, MACs between X and its shift,
-    MACs between the shift and the carry add into t0)."""
-    m_gap, x_gap, c_gap = spread
-    opm = [f"v_mad_u64_u32 {treg(k)}, vcc, %[a{k}], %[{mul}], {treg(k)}" for k, mul in pos]
-    seq = []
-    if pos and pos[0][0] == 0:
-        seq.append(opm.pop(0))
-    seq.append("v_mul_lo_u32 v10, v2, %[np]")
-    lead = opm[:m_gap]
-    seq += lead
-    if len(lead) < 2:
-        seq.append("s_nop 1")
-    seq.append("@BC@")
-    seq += opm[m_gap:]
-    red = [f"v_mad_u64_u32 {treg(j - 1)}, vcc, v11, %[n{j}], {treg(j)}" for j in range(1, LL)]
-    seq.append("v_mad_u64_u32 v[6:7], vcc, v11, %[n0], v[2:3]")
-    seq += red[:x_gap]
-    seq.append("v_alignbit_b32 v8, v7, v6, 27")
-    seq.append("v_lshrrev_b32 v9, 27, v7")
-    seq += red[x_gap:x_gap + c_gap]
-    seq.append("v_lshl_add_u64 v[2:3], v[8:9], 0, v[2:3]")
-    seq += red[x_gap + c_gap:]
-    seq.append("v_and_b32_dpp v4, v6, %[mk] row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1")
-    seq.append("v_mov_b32 v5, 0")
-    parts = []
-    for s_ in seq:
-        if s_ == "@BC@":
-            parts.append('"v_and_b32_dpp v11, v10, %[mk] " BC " row_mask:0xf bank_mask:0xf\\n\\t"')
-        else:
-            parts.append(f'"{s_}\\n\\t"')
-    return " ".join(parts)
+def gen(LL, LB):
+    def window(a):
+        return sq_window(LL, a)
 
-
-out = ["// Generated by tools/gen_mont27_asm.py -- do not edit.", "#pragma once"]
-out.append("#ifndef FPHE_FUSED_SPREAD")
-out.append("#define FPHE_FUSED_SPREAD 1")
-out.append("#endif")
-out.append("#define R27F_T_OPS(T) [t0p] \"+{v[2:3]}\"(T[0]), [t37p] \"+{v[4:5]}\"(T[37]), "
-           + ", ".join(f'[t{j}] "+v"(T[{j}])' for j in range(1, LL - 1)))
-out.append('#define R27F_CLOB "v6", "v7", "v8", "v9", "v10", "v11", "vcc", "memory"')
-# FPHE_FUSED_SPREAD selects the instruction spacing of the two dependency chains
-SPREADS = {0: (3, 2, 1), 1: (6, 8, 8)}
-for sp, spread in SPREADS.items():
-    out.append(f"#if FPHE_FUSED_SPREAD == {sp}")
-    out.append(f"#define R27F_ROW(BC) {fused([(k, 'b') for k in range(LL)], spread)}")
+    macros = []
+    row = "".join(f'"v_mad_u64_u32 %[t{j}], vcc, %[a{j}], %[b], %[t{j}]\\n\\t" ' for j in range(LL))
+    macros.append(("RG_OPROW", row))
+    red = '"v_mad_u64_u32 %[x], vcc, %[m], %[n0], %[t0]\\n\\t" '
+    red += "".join(f'"v_mad_u64_u32 %[t{j-1}], vcc, %[m], %[n{j}], %[t{j}]\\n\\t" ' for j in range(1, LL))
+    macros.append(("RG_REDROW", red))
     for a in range(LL):
-        pos = []
-        for s in range(WIN):
-            k = (a + s) % LL
-            mul = "bf" if s == 0 else ("bl" if s == WIN - 1 else "bm")
-            pos.append((k, mul))
-        pos.sort()
-        out.append(f"#define R27F_SQROW_{a}(BC) {fused(pos, spread)}")
+        body = "".join(f'"v_mad_u64_u32 %[t{k}], vcc, %[a{k}], %[{mul}], %[t{k}]\\n\\t" ' for k, mul in window(a))
+        macros.append((f"RG_SQROW_{a}", body))
+    macros.append(("RG_T_OPS(T)", ", ".join(f'[t{j}] "+v"(T[{j}])' for j in range(LL))))
+    macros.append(("RG_A_INS(A)", ", ".join(f'[a{j}] "v"(A[{j}])' for j in range(LL))))
+    macros.append(("RG_N_INS(N, C)", ", ".join(f'[n{j}] C(N({j}))' for j in range(LL))))
+
+    # ---- fused rows: operand MACs + m + reduction MACs + the X fix-up in ONE asm block ---
+    # The accumulator limbs 0 and LL-1 are pinned to v[2:3] / v[4:5] and the row's
+    # temporaries to v6..v11, so the block can address their 32-bit halves (inline asm has no
+    # sub-register syntax).  Order inside the block:
+    #   t0's operand MAC (if the row has one) -> v_mul_lo (m = t0 n' mod 2^LB, broadcast from
+    #   the element's lane 0 by the DPP AND) issued under the remaining operand MACs, then the
+    #   reduction MACs with X = m n0 + t0 first; X >> LB is added to the new t0 in the shadow
+    #   of the later MACs, and X mod 2^LB moves to the lane below's top limb with a DPP AND.
+    # Hazards honoured by construction: >= 2 VALU instructions between the VALU write of v10
+    # and its DPP read; X (v6) is written ~LL instructions before its DPP read.
+    # BC is the DPP broadcast control string for TPI (quad_perm:[0,0,0,0] / [0,0,2,2]).
+    def treg(k):
+        return "v[2:3]" if k == 0 else ("v[4:5]" if k == LL - 1 else f"%[t{k}]")
+
+    def fused(pos, spread):
+        m_gap, x_gap, c_gap = spread
+        opm = [f"v_mad_u64_u32 {treg(k)}, vcc, %[a{k}], %[{mul}], {treg(k)}" for k, mul in pos]
+        seq = []
+        if pos and pos[0][0] == 0:
+            seq.append(opm.pop(0))
+        seq.append("v_mul_lo_u32 v10, v2, %[np]")
+        lead = opm[:m_gap]
+        seq += lead
+        if len(lead) < 2:
+            seq.append("s_nop 1")
+        seq.append("@BC@")
+        seq += opm[m_gap:]
+        redm = [f"v_mad_u64_u32 {treg(j - 1)}, vcc, v11, %[n{j}], {treg(j)}" for j in range(1, LL)]
+        seq.append("v_mad_u64_u32 v[6:7], vcc, v11, %[n0], v[2:3]")
+        seq += redm[:x_gap]
+        seq.append(f"v_alignbit_b32 v8, v7, v6, {LB}")
+        seq.append(f"v_lshrrev_b32 v9, {LB}, v7")
+        seq += redm[x_gap:x_gap + c_gap]
+        seq.append("v_lshl_add_u64 v[2:3], v[8:9], 0, v[2:3]")
+        seq += redm[x_gap + c_gap:]
+        seq.append("v_and_b32_dpp v4, v6, %[mk] row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1")
+        seq.append("v_mov_b32 v5, 0")
+        parts = []
+        for s_ in seq:
+            if s_ == "@BC@":
+                parts.append('"v_and_b32_dpp v11, v10, %[mk] " BC " row_mask:0xf bank_mask:0xf\\n\\t"')
+            else:
+                parts.append(f'"{s_}\\n\\t"')
+        return " ".join(parts)
+
+    macros.append(("RGF_T_OPS(T)", f'[t0p] "+{{v[2:3]}}"(T[0]), [tlp] "+{{v[4:5]}}"(T[{LL - 1}]), '
+                   + ", ".join(f'[t{j}] "+v"(T[{j}])' for j in range(1, LL - 1))))
+    macros.append(("RGF_CLOB", '"v6", "v7", "v8", "v9", "v10", "v11", "vcc", "memory"'))
+    # FPHE_FUSED_SPREAD selects the instruction spacing of the two dependency chains
+    SPREADS = {0: (3, 2, 1), 1: (6, 8, 8)}
+    spread_macros = {}
+    for sp, spread in SPREADS.items():
+        lst = [("RGF_ROW(BC)", fused([(k, "b") for k in range(LL)], spread))]
+        for a in range(LL):
+            lst.append((f"RGF_SQROW_{a}(BC)", fused(window(a), spread)))
+        spread_macros[sp] = lst
+
+    out = [f"// Generated by tools/gen_mont27_asm.py -- do not edit.  {LL} limbs of {LB} bits per lane.",
+           "// No include guard: included once per section (RG_SECTION) by mont_engine.inc.",
+           "#if RG_SECTION == 1"]
+    for name, body in macros:
+        out.append(f"#define {name} {body}")
+    out.append("#ifndef FPHE_FUSED_SPREAD")
+    out.append("#define FPHE_FUSED_SPREAD 1")
     out.append("#endif")
-out.append("template <int a> __device__ __forceinline__ void r27f_sqrow(u64 (&T)[LL], const L27& A, u32 bf, u32 bm, u32 bl, const Mod<TPI_>& N, u32 np);")
-path = os.path.join(os.path.dirname(__file__), "..", "fate_amd", "csrc", "mont27_fused_gen.h")
-# dispatcher: r27f_sqrow<TPI, a>(T, A, bf, bm, bl, N, np, mk) (TPI 2 or 4)
-out.pop()
-out.append("template <int TPI> struct R27Bc;")
-out.append('template <> struct R27Bc<4> { static constexpr const char* s = "quad_perm:[0,0,0,0]"; };')
-out.append("template <int TPI, int a> __device__ __forceinline__ void r27f_sqrow(u64 (&T)[LL], const L27& A, u32 bf, u32 bm, u32 bl, const Mod<TPI>& N, u32 np, u32 mk);")
-for a in range(LL):
-    for tpi, bc in ((4, "quad_perm:[0,0,0,0]"), (2, "quad_perm:[0,0,2,2]")):
-        out.append(f"template <> __device__ __forceinline__ void r27f_sqrow<{tpi}, {a}>(u64 (&T)[LL], const L27& A, u32 bf, u32 bm, u32 bl, const Mod<{tpi}>& N, u32 np, u32 mk) {{")
-        out.append(f'  asm volatile(R27F_SQROW_{a}("{bc}") : R27F_T_OPS(T) : R27_A_INS(A), R27_N_INS(N, "v"), [bf] "v"(bf), [bm] "v"(bm), [bl] "v"(bl), [np] "s"(np), [mk] "v"(mk) : R27F_CLOB);')
+    for sp, lst in spread_macros.items():
+        out.append(f"#if FPHE_FUSED_SPREAD == {sp}")
+        for name, body in lst:
+            out.append(f"#define {name} {body}")
+        out.append("#endif")
+    out.append("#elif RG_SECTION == 2")
+    sig = "u64 (&T)[LL], const L27& A, u32 bf, u32 bm, u32 bl"
+    out.append(f"template <int a> __device__ __forceinline__ void r27_sqrow({sig});")
+    for a in range(LL):
+        out.append(f"template <> __device__ __forceinline__ void r27_sqrow<{a}>({sig}) {{")
+        out.append(f'  asm volatile(RG_SQROW_{a} : RG_T_OPS(T) : RG_A_INS(A), [bf] "v"(bf), [bm] "v"(bm), [bl] "v"(bl) : "vcc", "memory");')
         out.append("}")
-for tpi, bc in ((4, "quad_perm:[0,0,0,0]"), (2, "quad_perm:[0,0,2,2]")):
-    out.append(f"template <int TPI> __device__ __forceinline__ void r27f_row(u64 (&T)[LL], const L27& A, u32 b, const Mod<TPI>& N, u32 np, u32 mk);") if tpi == 4 else None
-    out.append(f"template <> __device__ __forceinline__ void r27f_row<{tpi}>(u64 (&T)[LL], const L27& A, u32 b, const Mod<{tpi}>& N, u32 np, u32 mk) {{")
-    out.append(f'  asm volatile(R27F_ROW("{bc}") : R27F_T_OPS(T) : R27_A_INS(A), R27_N_INS(N, "v"), [b] "v"(b), [np] "s"(np), [mk] "v"(mk) : R27F_CLOB);')
-    out.append("}")
-out = [l for l in out if not l.startswith("template <int TPI> struct R27Bc") and "R27Bc<4>" not in l]
-with open(path, "w") as f:
-    f.write("\n".join(out) + "\n")
+    out.append("#elif RG_SECTION == 3")
+    out.append("template <int TPI, int a> __device__ __forceinline__ void r27f_sqrow(u64 (&T)[LL], const L27& A, u32 bf, u32 bm, u32 bl, const Mod<TPI>& N, u32 np, u32 mk);")
+    tpis = ((4, "quad_perm:[0,0,0,0]"), (2, "quad_perm:[0,0,2,2]"))
+    for a in range(LL):
+        for tpi, bc in tpis:
+            out.append(f"template <> __device__ __forceinline__ void r27f_sqrow<{tpi}, {a}>(u64 (&T)[LL], const L27& A, u32 bf, u32 bm, u32 bl, const Mod<{tpi}>& N, u32 np, u32 mk) {{")
+            out.append(f'  asm volatile(RGF_SQROW_{a}("{bc}") : RGF_T_OPS(T) : RG_A_INS(A), RG_N_INS(N, "v"), [bf] "v"(bf), [bm] "v"(bm), [bl] "v"(bl), [np] "s"(np), [mk] "v"(mk) : RGF_CLOB);')
+            out.append("}")
+    out.append("template <int TPI> __device__ __forceinline__ void r27f_row(u64 (&T)[LL], const L27& A, u32 b, const Mod<TPI>& N, u32 np, u32 mk);")
+    for tpi, bc in tpis:
+        out.append(f"template <> __device__ __forceinline__ void r27f_row<{tpi}>(u64 (&T)[LL], const L27& A, u32 b, const Mod<{tpi}>& N, u32 np, u32 mk) {{")
+        out.append(f'  asm volatile(RGF_ROW("{bc}") : RGF_T_OPS(T) : RG_A_INS(A), RG_N_INS(N, "v"), [b] "v"(b), [np] "s"(np), [mk] "v"(mk) : RGF_CLOB);')
+        out.append("}")
+    out.append("#elif RG_SECTION == 4")
+    names = {n.split("(")[0] for n, _ in macros} | {n.split("(")[0] for lst in spread_macros.values() for n, _ in lst}
+    for n in sorted(names):
+        out.append(f"#undef {n}")
+    out.append("#endif")
+    path = os.path.join(HERE, "..", "fate_amd", "csrc", f"mont_gen_ll{LL}.h")
+    with open(path, "w") as f:
+        f.write("\n".join(out) + "\n")
+
+
+if __name__ == "__main__":
+    gen(38, 27)
+    gen(37, 28)
