@@ -35,6 +35,8 @@ KEY_FIXTURE = os.path.join(ROOT, "tests", "golden", "paillier_2048.json")
 # (measured half rate in profiles/r01_probe_alu.txt); one MAC32 = 32x32->64 multiply-add.
 PEAK_TMAC32 = 256 * 128 * 2.4e9 / 2 / 1e12
 PEAK_HBM_GBS = 8000.0
+# limbs per lane of the Montgomery engine (28-bit limbs, fate_amd/csrc/mont27_dev.h)
+ENGINE_LL = 37
 
 
 def mac32_per_mont(L: int) -> int:
@@ -87,12 +89,13 @@ def sliding_window_products(e: int, w: int = 6) -> int:
 def enc_mad27_per_elem(key_bits: int, n: int) -> float:
     # issued v_mad_u64_u32 of the reduced-radix engine (fate_amd/csrc/mont27_dev.h), summed
     # over an element's TPI lanes: a general product is NL rows x 2 NL MACs; a squaring
-    # (mont_sqr) NL rows x TPI x (20 + 38) MACs.  NL = 152 for 4096-bit n^2.
+    # (mont_sqr) NL rows x TPI x (LL/2 + 1 + LL) MACs.  28-bit limbs, LL = 37 per lane:
+    # NL = 148 for 4096-bit n^2 (mont27_dev.h).
     # Products: to-Montgomery, the sliding-window r^n, x C_nude.
-    NL = 38 * (key_bits // 16 // 32)
-    TPI = NL // 38
+    TPI = key_bits // 16 // 32
+    NL = ENGINE_LL * TPI
     sq, mul = sliding_window_schedule(n)
-    return (1 + mul + 1) * 2 * NL * NL + sq * NL * TPI * (20 + 38)
+    return (1 + mul + 1) * 2 * NL * NL + sq * NL * TPI * (ENGINE_LL // 2 + 1 + ENGINE_LL)
 
 
 def enc_crt_mac32_per_elem(key_bits: int) -> float:
@@ -201,16 +204,16 @@ def add_kernel_leg(P, pk, a, b, N, stream, dev) -> dict:
     L = a.L2
     mac = N * (1 + 4 * float(gaps.double().mean())) * mac32_per_mont(L)
     hist = torch.bincount(gaps.cpu()).tolist()
-    # issued 27-bit MACs: to-Montgomery + final product (general) and the wave-max squarings
-    NL = 38 * (L // 32)
-    TPI = NL // 38
+    # issued MACs: to-Montgomery + final product (general) and the wave-max squarings
+    TPI = L // 32
+    NL = ENGINE_LL * TPI
     per_wave = 64 // TPI
     gs = gaps[order.long()] if order is not None else gaps
     pad = (-N) % per_wave
     if pad:
         gs = torch.cat([gs, gs.new_zeros(pad)])
     wave_sq = 4 * gs.view(-1, per_wave).amax(1).double().sum().item() * per_wave
-    mads = N * 2 * 2 * NL * NL + wave_sq * NL * TPI * (20 + 38)
+    mads = N * 2 * 2 * NL * NL + wave_sq * NL * TPI * (ENGINE_LL // 2 + 1 + ENGINE_LL)
     blk = valu_roofline("k_add27<128> (exponent-gap order)", mac, ms, N * (3 * (L * 4 + 5) + 4),
                         per_elem_mac32=round(mac / N, 1), gap_histogram=hist, sorted=order is not None)
     blk["issue"] = {"mad64_per_elem": round(mads / N, 1), "achieved": round(mads / (ms / 1e3) / 1e12, 3),

@@ -585,7 +585,7 @@ template <int L>
 fphe_status launch_encrypt27(fphe_ctx* c, const uint32_t* P, uint32_t lp, const uint8_t* neg, size_t count, int obf,
                              const uint32_t* r, const uint32_t key[8], uint64_t nonce, uint32_t* C, uint8_t* sign,
                              hipStream_t s) {
-  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = rad_ll(TPI) * TPI, LDSW = NL > L ? NL : L, L1 = L / 2;
+  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = rad_ll(TPI) * TPI, LDSW = NL > L + 3 ? NL : L + 3, L1 = L / 2;
   auto kern = KS<TPI>::template encrypt<L, kWinSlide>();
   const size_t lds = (size_t)kWavesPerBlock * LDSW * E * 4;
   set_lds(kern, lds);
@@ -635,7 +635,7 @@ fphe_status launch_encrypt_crt27(fphe_ctx* c, const uint32_t* P, uint32_t lp, co
                                  const uint32_t* r, const uint32_t key[8], uint64_t nonce, uint32_t* C,
                                  uint8_t* sign, hipStream_t s) {
   constexpr int TPIh = L / 64, Eh = FPHE_WAVE / TPIh, NLh = rad_ll(TPIh) * TPIh, L1 = L / 2;
-  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = rad_ll(TPI) * TPI, LDSW = NL > L + 2 ? NL : L + 2;
+  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = rad_ll(TPI) * TPI, LDSW = NL > L + 3 ? NL : L + 3;
   auto k1 = KS<TPIh>::template pow_half<L, kWinSlide, true>();
   const size_t lds1 = (size_t)kWavesPerBlock * NLh * Eh * 4;
   set_lds(k1, lds1);

@@ -175,8 +175,8 @@ using namespace fphe::r28;
 #include "kernels_engine.inc"
 }  // namespace k28
 
-// 27-bit limbs at TPI = 4 (4096-bit moduli), 28-bit at TPI 1 and 2 (mont27_dev.h)
+// the radix namespace of a TPI (mont27_dev.h rad_lb: 28 everywhere unless FPHE_RADIX4=27)
 template <int TPI>
-using KS = std::conditional_t<TPI == 4, k27::Kern, k28::Kern>;
+using KS = std::conditional_t<fphe::rad_lb(TPI) == 27, k27::Kern, k28::Kern>;
 
 }  // namespace

@@ -24,14 +24,14 @@
 // to its canonical residue with one subtraction.
 //
 // Two radices, one engine text (mont_engine.inc, inv_engine.inc) compiled in two namespaces:
-//   r27: 27-bit limbs, 38 per lane (1026 bits) -- TPI = 4, the 4096-bit n^2 of 2048-bit keys:
-//        a column takes <= 2 x 152 products < 2^54, < 2^62.3;
-//   r28: 28-bit limbs, 37 per lane (1036 bits) -- TPI = 1, 2, every modulus up to 2048 bits
-//        (p^2, q^2 and n of 2048-bit keys; all moduli of <= 1024-bit keys): a column takes
-//        <= 2 x 74 products < 2^56.01, < 2^63.3.  74 limbs instead of 76 cut the MACs of a
-//        product by (74/76)^2 and a squaring row to 19 + 37 MACs (odd LL: no half-window
-//        column), against 20 + 38.  At TPI = 4, 28-bit limbs would overflow a 64-bit column
-//        (2 x 148 x 2^56 > 2^64), so the 4096-bit engine stays at 27 bits.
+//   r28: 28-bit limbs, 37 per lane (1036 bits) -- every modulus (the engine in use): a
+//        product is < 2^56 and a column takes <= 3 products per row span; at NL <= 74 that
+//        fits 64 bits outright (< 2^63.8), at NL = 148 (TPI 4, the 4096-bit n^2 of 2048-bit
+//        keys) a carry sweep after half the rows bounds the slots again (mont_engine.inc
+//        sweep()).  37 limbs per lane instead of 38 cut a product's MACs by (NL'/NL)^2 and a
+//        squaring row to 19 + 37 MACs (odd LL: no half-window column), against 20 + 38.
+//   r27: 27-bit limbs, 38 per lane (1026 bits) -- round 1's engine, no sweep needed
+//        (< 2^62.3 at NL = 152); kept for same-box A/B (FPHE_RADIX4=27 builds TPI 4 on it).
 // kernels27.h instantiates every kernel in both and the launchers pick by TPI (KS<TPI>).
 #pragma once
 #include "mont_dev.h"
@@ -77,7 +77,11 @@ constexpr int LL = 37;
 #undef RG_GEN_FILE
 }  // namespace r28
 
-// limb geometry of the engine a TPI runs on (host and device)
-constexpr int rad_lb(int tpi) { return tpi == 4 ? 27 : 28; }
-constexpr int rad_ll(int tpi) { return tpi == 4 ? 38 : 37; }
+// limb geometry of the engine a TPI runs on (host and device): 28 x 37, or 27 x 38 for the
+// 4096-bit geometry when built with FPHE_RADIX4=27
+#ifndef FPHE_RADIX4
+#define FPHE_RADIX4 28
+#endif
+constexpr int rad_lb(int tpi) { return tpi == 4 ? FPHE_RADIX4 : 28; }
+constexpr int rad_ll(int tpi) { return rad_lb(tpi) == 27 ? 38 : 37; }
 }  // namespace fphe
