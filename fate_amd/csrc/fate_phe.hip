@@ -693,13 +693,18 @@ fphe_status launch_add27(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, con
   set_lds(kern, lds);
   const size_t cmax = add_max_count(L);
   if (ord && count > cmax) return FPHE_ERR_ARG;  // an order must stay inside one addressable chunk
+  if (count == 0) return FPHE_OK;
+  // the kernel's wave-tile counter lives in the context scratch (stream-owned, see ensure_scratch)
+  if (ensure_scratch(c, 256, s) != FPHE_OK) return FPHE_ERR_HIP;
+  u32* next_tile = c->scratch;
   for (size_t s0 = 0; s0 < count; s0 += cmax) {  // whole tiles per chunk: pointer offsets stay tile-aligned
     const size_t n = count - s0 < cmax ? count - s0 : cmax;
     const size_t wo = s0 / FPHE_WAVE * L * FPHE_WAVE;  // word offset of the chunk's first tile
     const unsigned grid = occ_grid(c, kern, lds, (n + E - 1) / E, "add27");
+    if (hipMemsetAsync(next_tile, 0, sizeof(u32), s) != hipSuccess) return FPHE_ERR_HIP;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, Ca + wo, sa + s0, ea + s0,
                        bstride ? Cb + wo : Cb, bstride ? sb + s0 : sb, bstride ? eb + s0 : eb, bstride, n, ord,
-                       Co + wo, so + s0, eo + s0, (u32)NL);
+                       Co + wo, so + s0, eo + s0, next_tile, (u32)NL);
   }
   return hip_ok(hipGetLastError());
 }
