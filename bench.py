@@ -490,6 +490,8 @@ def main() -> None:
         gw = torch.Generator().manual_seed(777 + rank)
         wts = (torch.rand(N, generator=gw, dtype=torch.float32) * 3.0 - 1.0).to(dev)
         pw = coder.encode_f32_vec(wts)
+        n_neg = int((wts < 0).sum().item())
+        ct.mul(pk, pw)  # untimed: grows the context scratch to the op's size
         torch.cuda.synchronize(dev)
         e0.record(stream)
         m = ct.mul(pk, pw)
@@ -618,6 +620,12 @@ def main() -> None:
                                          N * dec_mac32_per_elem(key_bits), dec_ms,
                                          N * (key_bits // 4 + 4 + key_bits // 8)),
                 "ct_add": add_kernel,
+                # §8(d): float significands (E = 56): (56 + 12 + 16) mulmods over L = 128, + 3
+                # for each negative weight (the inverse branch); the whole op is timed:
+                # classify, batch inverse of the negative-weight elements, the powm
+                "ct_mul": valu_roofline("k_mul_prep + k_binv_pre27/k_inv_n27/k_inv_lift27/k_binv_post27 + k_mul27<128,4>",
+                                        (N * (56 + 12 + 16) + 3 * n_neg) * mac32_per_mont(key_bits // 16), mul_ms,
+                                        N * 2 * (key_bits // 4 + 5) + N * 13, negative_weights=n_neg),
             },
         }
         del pt, y, ct2, s, ce, Ch, m, gh, hist

@@ -16,6 +16,7 @@ print("decrypt", d["decrypt_per_s"], d["rooflines"]["decrypt"]["frac"], d["roofl
 print("ct_add", d["ct_add_per_s"], d["rooflines"]["ct_add"]["frac"], d["rooflines"]["ct_add"]["kernel_ms"])
 print("keyholder", d["encrypt_keyholder_crt_per_s"], d["encrypt_keyholder_crt_roofline_frac"])
 print("key_1024", d["key_1024"])
-print("mul", d["ct_mul_per_s"])
+print("mul", d["ct_mul_per_s"], d["rooflines"]["ct_mul"]["frac"], d["rooflines"]["ct_mul"]["kernel_ms"])
+print("hist", d["histogram_scatter_adds_per_s"], "hlr", d["hetero_lr_gradient"])
 PY
 echo all_ok
