@@ -721,6 +721,20 @@ fphe_status launch_sqmul27(fphe_ctx* c, const uint32_t* Ca, const uint32_t* Cb, 
   return hip_ok(hipGetLastError());
 }
 
+template <int L>
+fphe_status launch_align27(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, const int32_t* gap, size_t count,
+                           uint32_t* Co, uint8_t* so, hipStream_t s) {
+  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = rad_ll(TPI) * TPI;
+  auto kern = KS<TPI>::template align<L>();
+  const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
+  set_lds(kern, lds);
+  if (ensure_scratch(c, 256, s) != FPHE_OK) return FPHE_ERR_HIP;  // the wave-tile counter
+  if (hipMemsetAsync(c->scratch, 0, sizeof(u32), s) != hipSuccess) return FPHE_ERR_HIP;
+  const unsigned grid = occ_grid(c, kern, lds, (count + E - 1) / E, "align27");
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, Ca, sa, gap, count, Co, so, c->scratch, (u32)NL);
+  return hip_ok(hipGetLastError());
+}
+
 // X0: scratch of ntiles * L1 * 64 words (the mod-n inverses between the two kernels)
 template <int L>
 void launch_inv27(fphe_ctx* c, const uint32_t* Ca, size_t count, const uint8_t* need, uint32_t* Co,
@@ -1463,6 +1477,18 @@ fphe_status fphe_sqmul(fphe_ctx* c, const uint32_t* Ca, const uint32_t* Cb, cons
   DevGuard g(c->device);
   if (c->L2 == 128) return launch_sqmul27<128>(c, Ca, Cb, sb, (int)nsq, count, Co, so, (hipStream_t)stream);
   return launch_sqmul27<64>(c, Ca, Cb, sb, (int)nsq, count, Co, so, (hipStream_t)stream);
+}
+
+
+fphe_status fphe_align(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, const int32_t* gap, size_t count,
+                       uint32_t* Co, uint8_t* so, void* stream) {
+  if (!c) return FPHE_ERR_ARG;
+  if (count == 0) return FPHE_OK;
+  if (!Ca || !sa || !gap || !Co || !so) return FPHE_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DevGuard g(c->device);
+  if (c->L2 == 128) return launch_align27<128>(c, Ca, sa, gap, count, Co, so, (hipStream_t)stream);
+  return launch_align27<64>(c, Ca, sa, gap, count, Co, so, (hipStream_t)stream);
 }
 
 

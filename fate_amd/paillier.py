@@ -1013,7 +1013,10 @@ def _fold_segments(pk: "PK", src: CiphertextVector, seg: torch.Tensor, index: Op
     cur, ckeys = _fold_chunks(pk, src, index[order], key)
     while bool((ckeys[1:] == ckeys[:-1]).any()):
         cur, ckeys = _fold_chunks(pk, cur, torch.arange(cur.count, device=dev), ckeys)
-    res, ids = _fold_tree(pk, cur, ckeys >> 32)
+    if MERGE_BY_ALIGN:
+        res, ids = _merge_exponents(pk, cur, ckeys)
+    else:
+        res, ids = _fold_tree(pk, cur, ckeys >> 32)
     # A segment whose terms are all the literal 1 folds to 1: add(1, y) returns y, so the
     # reference's sequential fold ends on its LAST term, exponent included (lib.rs:303-308).
     lit = _is_literal_one(res)
@@ -1031,6 +1034,62 @@ def _is_literal_one(v: CiphertextVector) -> torch.Tensor:
     C = v.C
     lit = ((C[:, 0, :] == 1) & (C[:, 1:, :] == 0).all(dim=1)).reshape(-1)[: v.count]
     return lit & (v.sign[: v.count] == 0)
+
+
+# merge a segment's per-exponent partials by one alignment pass + product folds (True), or by
+# the pairwise ct-add tree (False: ceil(log2(partials)) launches, each as long as its largest
+# exponent gap)
+MERGE_BY_ALIGN = True
+
+
+def _merge_exponents(pk: "PK", cur: CiphertextVector, ckeys: torch.Tensor) -> Tuple[CiphertextVector, torch.Tensor]:
+    """One ciphertext per segment from its per-exponent partials (keys (segment << 32) |
+    (exp + 2^31), ascending, one partial per key).  The reference's sequential adds raise
+    every term to 16^(e - e_min), e_min the least exponent of the segment's non-literal
+    terms, and multiply (decrese_exp_to + add, fixedpoint_paillier/src/lib.rs:250-258,
+    301-333; order-independent); a term that was raised loses its sign
+    (powm is canonical), so the product's sign is the XOR over the e_min terms.  Literal-1
+    partials are add's identity: they stay out of e_min and fold as 1.  So: one fphe_align
+    pass over all partials (largest gaps first), then plain product folds (fphe_fold) of
+    each segment, all at e_min.  Segments of literal-1 partials only fold to 1 (the caller
+    restores the reference's exponent for those)."""
+    dev = cur.device
+    n = cur.count
+    seg = ckeys >> 32
+    exp = (ckeys & 0xFFFFFFFF) - (1 << 31)
+    lit = _is_literal_one(cur)
+    big = 1 << 40
+    _, inv = torch.unique_consecutive(seg, return_inverse=True)
+    emin = torch.full((int(inv.max()) + 1,), big, dtype=torch.long, device=dev)
+    emin.scatter_reduce_(0, inv, torch.where(lit, torch.full_like(exp, big), exp), reduce="amin")
+    em = emin[inv]
+    gap = torch.where(lit | (em == big), torch.zeros_like(exp), exp - em)
+    tgt = torch.where(em == big, torch.zeros_like(em), em)
+    order = torch.argsort(gap, descending=True, stable=True)
+    src = cur._gather(order)
+    aligned = _align(pk, src, gap[order])
+    aligned.exp[:n] = tgt[order].to(torch.int32)
+    key2, o2 = torch.sort(seg[order] * (1 << 32) + (tgt[order] + (1 << 31)))
+    res, k2 = _fold_chunks(pk, aligned, o2, key2)
+    while bool((k2[1:] == k2[:-1]).any()):
+        res, k2 = _fold_chunks(pk, res, torch.arange(res.count, device=dev), k2)
+    return res, k2 >> 32
+
+
+def _align(pk: "PK", a: CiphertextVector, gap: torch.Tensor) -> CiphertextVector:
+    """(a^(16^gap) mod n^2, sign 0 where gap > 0, exp unchanged) on the device (fphe_align)."""
+    dev = a.device
+    a = _fit_limbs(a, pk._key.L2)
+    n = a.count
+    out = CiphertextVector.empty(n, a.L2, dev)
+    if n == 0:
+        return out
+    out.exp[:n] = a.exp[:n]
+    g32 = gap.to(device=dev, dtype=torch.int32).contiguous()
+    lib = _lib.load()
+    _lib.check(lib.fphe_align(pk._key.ctx(dev), _ptr(a.C), _ptr(a.sign), _ptr(g32), n, _ptr(out.C), _ptr(out.sign),
+                              ctypes.c_void_p(_stream(dev))), "fphe_align")
+    return out
 
 
 def _fold_tree(pk: "PK", src: CiphertextVector, seg: torch.Tensor) -> Tuple[CiphertextVector, torch.Tensor]:

@@ -201,6 +201,17 @@ fphe_status fphe_fold(fphe_ctx* ctx, const uint32_t* Src, const uint8_t* ssign, 
 fphe_status fphe_sqmul(fphe_ctx* ctx, const uint32_t* Ca, const uint32_t* Cb, const uint8_t* sb, uint32_t nsq,
                        size_t count, uint32_t* Co, uint8_t* so, void* stream);
 
+/* Co = Ca^(16^gap[i]) mod n^2 per element (gap >= 0), so = 0 where gap > 0 (canonical powm),
+ * sa where gap == 0 (copied through): the exponent-alignment step of Ciphertext::add,
+ * decrese_exp_to (fixedpoint_paillier/src/lib.rs:250-258), for many elements at once.  The
+ * reference aligns pairwise inside its sequential folds (iupdate, intervals_sum, matmul,
+ * lib.rs:521-791); aligning every per-exponent partial of a fold segment to the segment's
+ * minimum exponent and multiplying gives the same integers (the fold is order-independent).
+ * Elements in descending-gap order run fastest (a wave pays its largest gap).  gap is a
+ * flat int32 array; C arrays tile-major as fphe_add. */
+fphe_status fphe_align(fphe_ctx* ctx, const uint32_t* Ca, const uint8_t* sa, const int32_t* gap, size_t count,
+                       uint32_t* Co, uint8_t* so, void* stream);
+
 /* Element permutation of tile-major vectors: the data movement under CiphertextVector.slice /
  * slice_indexes / cat / i_shuffle / shuffle / iupdate and the fold plumbing (paillier.rs:
  * 228-300; fixedpoint_paillier/src/lib.rs:452-509).  scatter = 0: out[i] = in[idx[i]];
