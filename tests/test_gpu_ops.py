@@ -234,6 +234,49 @@ def test_iupdate_long_segments(env):
     assert host(pk, v) == ref(want)
 
 
+def test_align_many_gaps(env):
+    """fphe_align (the per-exponent merge of the folds): c^(16^gap) mod n^2, canonical with
+    sign 0 for gap > 0 (decrese_exp_to, lib.rs:250-258), the element unchanged for gap 0;
+    gaps 0..31 mixed within waves, signed inputs, the literal 1, a ragged tail."""
+    fx, sk, pk, coder, opk, cts = env
+    rng = random.Random(21)
+    terms = more(opk, cts, 131, seed=4)
+    terms[7] = O.ct_zero()
+    gaps = [rng.choice([0, 0, 1, 2, 3, 5, 9, 17, 31]) for _ in terms]
+    got = P._align(pk, dev_vec(pk, terms), torch.tensor(gaps))
+    want = []
+    for t, g in zip(terms, gaps):
+        if g == 0:
+            want.append((t.c, t.exp))
+        else:
+            want.append((pow(t.c % opk.ns, 16 ** g, opk.ns), t.exp))
+    assert host(pk, got) == want
+
+
+def test_iupdate_wide_exponents(env):
+    """Slots whose terms span exponents -40..4 (gaps up to 44, 176 squarings), with literal
+    1s whose exponent is below every other term of their slot (a literal 1 is add's
+    identity and must not set the slot's exponent), against the sequential fold."""
+    fx, sk, pk, coder, opk, cts = env
+    rng = random.Random(23)
+    other = []
+    for i in range(300):
+        c = rng.randrange(2, opk.ns)
+        other.append(O.Ciphertext(-c if rng.random() < 0.4 else c, rng.randrange(-40, 5)))
+    for i in (3, 50, 77):
+        other[i] = O.Ciphertext(1, -60)  # literal 1, lowest exponent of any term
+    data = [O.ct_zero() for _ in range(6)]
+    data[4] = cts[3]
+    indexes = [[rng.randrange(6)] for _ in range(len(other))]
+    indexes[3] = [5]
+    indexes[50] = [5]  # slot 5: literal 1s and what else lands there
+    v = dev_vec(pk, data)
+    v.iupdate(dev_vec(pk, other), indexes, 1, pk)
+    want = list(data)
+    O.iupdate(opk, want, other, indexes, 1)
+    assert host(pk, v) == ref(want)
+
+
 def test_chunking_cumsum_with_step(env):
     fx, sk, pk, coder, opk, cts = env
     data = cts[:24]
