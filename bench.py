@@ -320,12 +320,16 @@ def launch_ranks(nproc: int) -> int:
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    # torchrun's own parser would take "--n" as an abbreviation of its options: pass --elements
-    args = ["--elements" if a == "--n" else ("--elements=" + a[4:] if a.startswith("--n=") else a)
-            for a in sys.argv[1:]]
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
-           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + args
-    return subprocess.call(cmd)
+    return subprocess.call(rank_command(nproc, port, sys.argv[1:]))
+
+
+def rank_command(nproc: int, port: int, argv) -> list:
+    """The torch.distributed.run command line launch_ranks starts: one node, `nproc` ranks,
+    rendezvous on 127.0.0.1:port, this script with the same arguments.  torchrun's own
+    parser would take "--n" as an abbreviation of its options, so it is passed as --elements."""
+    args = ["--elements" if a == "--n" else ("--elements=" + a[4:] if a.startswith("--n=") else a) for a in argv]
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + args
 
 
 def main() -> None:
