@@ -132,7 +132,8 @@ def gen(LL, LB):
     out.append(f"template <int a> __device__ __forceinline__ void r27_sqrow({sig});")
     for a in range(LL):
         out.append(f"template <> __device__ __forceinline__ void r27_sqrow<{a}>({sig}) {{")
-        out.append(f'  asm volatile(RG_SQROW_{a} : RG_T_OPS(T) : RG_A_INS(A), [bf] "v"(bf), [bm] "v"(bm), [bl] "v"(bl) : "vcc", "memory");')
+        bl_in = ', [bl] "v"(bl)' if LL % 2 == 0 else ''  # odd LL: no half-window column, bl unused
+        out.append(f'  asm volatile(RG_SQROW_{a} : RG_T_OPS(T) : RG_A_INS(A), [bf] "v"(bf), [bm] "v"(bm){bl_in} : "vcc", "memory");')
         out.append("}")
     out.append("#elif RG_SECTION == 3")
     out.append("template <int TPI, int a> __device__ __forceinline__ void r27f_sqrow(u64 (&T)[LL], const L27& A, u32 bf, u32 bm, u32 bl, const Mod<TPI>& N, u32 np, u32 mk);")
@@ -140,7 +141,8 @@ def gen(LL, LB):
     for a in range(LL):
         for tpi, bc in tpis:
             out.append(f"template <> __device__ __forceinline__ void r27f_sqrow<{tpi}, {a}>(u64 (&T)[LL], const L27& A, u32 bf, u32 bm, u32 bl, const Mod<{tpi}>& N, u32 np, u32 mk) {{")
-            out.append(f'  asm volatile(RGF_SQROW_{a}("{bc}") : RGF_T_OPS(T) : RG_A_INS(A), RG_N_INS(N, "v"), [bf] "v"(bf), [bm] "v"(bm), [bl] "v"(bl), [np] "s"(np), [mk] "v"(mk) : RGF_CLOB);')
+            bl_in = ' [bl] "v"(bl),' if LL % 2 == 0 else ''
+            out.append(f'  asm volatile(RGF_SQROW_{a}("{bc}") : RGF_T_OPS(T) : RG_A_INS(A), RG_N_INS(N, "v"), [bf] "v"(bf), [bm] "v"(bm),{bl_in} [np] "s"(np), [mk] "v"(mk) : RGF_CLOB);')
             out.append("}")
     out.append("template <int TPI> __device__ __forceinline__ void r27f_row(u64 (&T)[LL], const L27& A, u32 b, const Mod<TPI>& N, u32 np, u32 mk);")
     for tpi, bc in tpis:
