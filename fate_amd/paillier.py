@@ -887,24 +887,13 @@ def _add_order(ea: torch.Tensor, eb: torch.Tensor, L2: int) -> Optional[torch.Te
     With float data the gaps differ from element to element, so most waves pay for an
     outlier; sorted by gap, a wave's elements need the same number of squarings.  The kernel
     reads and writes the elements in place through the order (no gather or scatter
-    copies), so the only cost is the sort.  Returns the (stable) int32 permutation, or None
-    when it would save less than 5% of the modular products."""
+    copies), and the order is a stable one-byte-key sort on the device (largest gaps first,
+    so the few long waves start at the head of the grid; gaps past 63 share the first
+    bucket): no host synchronisation, ~0.1 ms per 1M elements.  Returns the int32
+    permutation."""
     d = (ea.to(torch.int32) - eb.to(torch.int32)).abs()
-    per_wave = WAVE // (L2 // 32)  # elements per wave: TPI = L2/32 lanes per element
-    pad = (-d.numel()) % per_wave
-
-    def cost(x: torch.Tensor) -> torch.Tensor:
-        if pad:
-            x = torch.cat([x, x.new_zeros(pad)])
-        return (2 + 4 * x.view(-1, per_wave).amax(1)).sum()
-
-    # largest gaps first: the few long waves (a 0.0 against a large value can differ by 30
-    # exponent steps, 120 squarings) start at the head of the grid instead of trailing it
-    ds, order = torch.sort(d, stable=True, descending=True)
-    c = torch.stack([cost(d), cost(ds)]).tolist()
-    if c[1] > 0.95 * c[0]:
-        return None
-    return order.to(torch.int32)
+    key = (63 - d.clamp(max=63)).to(torch.uint8)
+    return torch.sort(key, stable=True)[1].to(torch.int32)
 
 
 def _add(pk: "PK", a: CiphertextVector, b: CiphertextVector, broadcast: bool, count: Optional[int] = None,
