@@ -126,6 +126,25 @@ def pmc_traffic_per_elem():
     return float(d["hbm_bytes_per_elem"]), os.path.relpath(paths[-1], ROOT)
 
 
+def pmc_ops_traffic(op: str):
+    """HBM bytes per element of the decrypt ("decrypt") or ct-add ("ct_add") kernels from the
+    committed PMC passes (tools/pmc_ops_summary.py), or (None, None)."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "*pmc_ops.json"), recursive=True),
+                   key=os.path.basename)
+    if not paths:
+        return None, None
+    with open(paths[-1]) as f:
+        d = json.load(f)
+    return float(d[op]["hbm_bytes_per_elem"]), os.path.relpath(paths[-1], ROOT)
+
+
+def _traffic(op: str, n: int):
+    """roofline.traffic for n elements of op (HBM bytes per launch from the PMC profile)."""
+    b, _ = pmc_ops_traffic(op)
+    return None if b is None else round(b * n)
+
+
 def cpu_baseline(p: int, q: int, seconds: float = 3.0):
     """The libgmp restatement of the reference's per-element call sequence (oracle/gmp_ref.c)
     timed the way FATE runs it: one worker process per core (oracle/cpu_baseline.py), for
@@ -622,8 +641,10 @@ def main() -> None:
             "rooflines": {
                 "decrypt": valu_roofline("k_pow_half27<128,6,false> + k_decrypt_crt<128>",
                                          N * dec_mac32_per_elem(key_bits), dec_ms,
-                                         N * (key_bits // 4 + 4 + key_bits // 8)),
-                "ct_add": add_kernel,
+                                         N * (key_bits // 4 + 4 + key_bits // 8),
+                                         traffic=_traffic("decrypt", N), traffic_source=pmc_ops_traffic("decrypt")[1]),
+                "ct_add": dict(add_kernel, traffic=_traffic("ct_add", N),
+                               traffic_source=pmc_ops_traffic("ct_add")[1]),
                 # §8(d): float significands (E = 56): (56 + 12 + 16) mulmods over L = 128, + 3
                 # for each negative weight (the inverse branch); the whole op is timed:
                 # classify, batch inverse of the negative-weight elements, the powm

@@ -1,0 +1,53 @@
+"""HBM traffic of the decrypt and ct-add kernels from FETCH_SIZE / WRITE_SIZE passes over
+tools/bench_legs/ops_pmc_leg.py (tools/gpu_job_ops_traffic.sh): decrypt of 2^18 elements
+(k_pow_half27<128, 6, false> + k_decrypt_crt<128>), the Hetero-LR-shaped ct-add of 2^20
+(k_add27<128>), 2048-bit key.  FETCH_SIZE doubled per the calibration probe
+(tools/probe/fetch_calib.hip: one dword per lane over 256-B rows, the pattern of these
+kernels' ColIO / whole-vector descriptor accesses).  bench.py reports the result as the
+`traffic` of rooflines.decrypt / rooflines.ct_add.
+
+    python tools/pmc_ops_summary.py gpurun_out/TAG profiles/r02/TAG_pmc_ops.json
+"""
+import collections
+import csv
+import json
+import sys
+
+KERNELS = {"decrypt": (["k_pow_half27<128, 6, false>", "k_decrypt_crt<128>"], 1 << 18,
+                       "algorithmic: read 512 B C (+ sign/exp), write 4-256 B plaintext"),
+           "ct_add": (["k_add27<128>"], 1 << 20, "algorithmic: two 517-B operands read, one written (+4-B order)")}
+
+
+def per_kernel(path, counter):
+    agg = collections.defaultdict(float)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] == counter:
+            agg[(r["Kernel_Name"], r["Dispatch_Id"])] += float(r["Counter_Value"])
+    return agg
+
+
+def main(prefix, out):
+    f = per_kernel(f"{prefix}_fetch/run_counter_collection.csv", "FETCH_SIZE")
+    w = per_kernel(f"{prefix}_write/run_counter_collection.csv", "WRITE_SIZE")
+    res = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over tools/bench_legs/ops_pmc_leg.py",
+           "calibration": {"fetch_bytes_per_counted_byte": 2.0, "write_bytes_per_counted_byte": 1.0}}
+    for name, (kerns, elems, note) in KERNELS.items():
+        rd = wr = 0.0
+        detail = {}
+        for k in kerns:
+            fk = [v for (kn, _), v in f.items() if k in kn]
+            wk = [v for (kn, _), v in w.items() if k in kn]
+            if len(fk) != 1 or len(wk) != 1:
+                raise SystemExit(f"expected one {k} dispatch per pass, found {len(fk)}/{len(wk)}")
+            detail[k] = {"FETCH_SIZE_KiB": fk[0], "WRITE_SIZE_KiB": wk[0]}
+            rd += fk[0] * 1024 * 2.0
+            wr += wk[0] * 1024
+        res[name] = {"kernels": detail, "elements": elems, "hbm_read_bytes_per_elem": round(rd / elems, 1),
+                     "hbm_write_bytes_per_elem": round(wr / elems, 1),
+                     "hbm_bytes_per_elem": round((rd + wr) / elems, 1), "note": note}
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps({k: v.get("hbm_bytes_per_elem") for k, v in res.items() if isinstance(v, dict) and "elements" in v}))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])

@@ -36,8 +36,8 @@ def main(prefix: str, out: str, elements: int = 131072, kernel: str = "k_encrypt
                         "fetch_bytes_per_counted_byte": 2.0, "write_bytes_per_counted_byte": 1.0},
         "hbm_read_bytes_per_elem": round(rd, 1),
         "hbm_write_bytes_per_elem": round(wr, 1),
-        "note": "dominated by the per-wave sliding-window table in global scratch (33 entries x 608 B per element "
-                "written, one 608-B entry read per window product); algorithmic traffic is 526 B/element",
+        "note": "dominated by the per-wave sliding-window table in global scratch (33 entries x 592 B per element "
+                "written, one 592-B entry read per window product); algorithmic traffic is 526 B/element",
         "hbm_bytes_per_elem": round(rd + wr, 1),
     }
     with open(out, "w") as f:
