@@ -286,3 +286,49 @@ def test_unsupported_key_sizes_decline():
         PR.keygen(3072)
     with pytest.raises(AssertionError):
         P.keygen(1023)
+
+
+@pytest.mark.parametrize("bits", [1024, 2048])
+def test_extreme_operands(bits):
+    """Operands at the edges of the 28-bit engine's bounds (all-ones limbs, n^2 - 1, 2^k - 1
+    just under n^2, 2, the literal 1) through ct-add with exponent gaps, ct x pt by small,
+    big (n - small: a full-size exponent) and negative plaintexts, neg, the exponent
+    alignment and decrypt; obfuscated encryption with r = 1 and r = n - 1 of the largest and
+    smallest encodable significands.  Bit-exact against the oracle."""
+    p, q, sk, pk, coder, osk, opk = load(bits)
+    ns, n = opk.ns, opk.n
+    L = ns.bit_length()
+    m28 = (L - 1) // 28
+    vals = [2, ns - 1, ns - 2, (ns - 1) // 2, (1 << (L - 1)) - 1, (1 << (28 * m28)) - 1,
+            ns - (1 << (28 * (m28 - 1))), int("5" * (L // 4 - 1), 16) % ns, 1]
+    signs = [0, 1, 0, 1, 0, 0, 1, 0, 0]
+    cts = [O.Ciphertext(-(ns - v) if s else v, e) for v, s, e in zip(vals, signs, [0, -3, 2, 0, -1, 0, 5, -2, 0])]
+    other = [O.Ciphertext(v, e) for v, e in zip(reversed(vals), [1, 0, -3, 4, 0, -1, 0, 0, 3])]
+    dv = P.CiphertextVector.from_signed_ints([c.c for c in cts], [c.exp for c in cts], pk.ns, pk._key.L2)
+    dw = P.CiphertextVector.from_signed_ints([c.c for c in other], [c.exp for c in other], pk.ns, pk._key.L2)
+
+    def host(v):
+        cs, es = v.to_signed_ints(pk.ns)
+        return list(zip(cs, es))
+
+    assert host(dv.add(pk, dw)) == [(c.c, c.exp) for c in (O.ct_add(opk, a, b) for a, b in zip(cts, other))]
+    assert host(dv.neg(pk)) == [(c.c, c.exp) for c in (O.ct_neg(opk, a) for a in cts)]
+    pts = [O.Plaintext(v, e) for v, e in zip([3, n - 5, n - 1, n // 2, 1, 0, 7, (1 << 60) + 1, 2],
+                                             [0, 0, 1, -1, 0, 0, 0, -2, 0])]
+    pv = P.PlaintextVector.from_ints([t.significant for t in pts], [t.exp for t in pts])
+    assert host(dv.mul(pk, pv)) == [(c.c, c.exp) for c in (O.ct_mul(opk, a, t) for a, t in zip(cts, pts))]
+    gaps = [5, 0, 1, 31, 2, 0, 3, 9, 4]
+    al = P._align(pk, dv, torch.tensor(gaps))
+    assert host(al) == [((c.c if g == 0 else pow(c.c % ns, 16 ** g, ns)), c.exp) for c, g in zip(cts, gaps)]
+    sig, _ = sk.decrypt_to_encoded(dv).to_ints()
+    assert sig == [O.decrypt(osk, c.c) for c in cts]
+    # obfuscated encryption at the significand edges with r = 1 and r = n - 1 (a significand
+    # above n/4 takes the reference's invert branch)
+    maxi = n // 2
+    sigs = [maxi, -maxi, 1, -1, 0, maxi - 1, n // 4, n // 4 + 1]
+    rs = [1, n - 1, n - 1, 1, n - 1, 2, 1, n - 1]
+    want = [O.fp_encrypt(opk, O.Plaintext(sg, 0), True, r) for sg, r in zip(sigs, rs)]
+    pk_pub = P.keypair_from_primes(p, q, keyholder=False)[1]
+    for k in (pk, pk_pub):  # key-holder CRT path and public-key path
+        enc = k.encrypt_encoded(P.PlaintextVector.from_ints(sigs, [0] * len(sigs)), True, r=rs)
+        assert host(enc) == [(c.c, c.exp) for c in want]
