@@ -54,7 +54,7 @@ __device__ __forceinline__ void cs_step(int (&v)[16], int& prev, int h) {
 
 extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_redc7(
     const v4i* __restrict__ Afrag, const int8_t* __restrict__ T, int* __restrict__ U, int nelem, int reps,
-    int* __restrict__ dbg) {
+    int* __restrict__ dbg, int shared_t) {
   __shared__ v4i sA[(NA1 + NA2) * 64];
   for (int i = threadIdx.x; i < (NA1 + NA2) * 64; i += blockDim.x) sA[i] = Afrag[i];
   __syncthreads();
@@ -64,8 +64,10 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
   const int nbatch = nelem / 32;
   for (int b = wave; b < nbatch; b += nwaves) {
     const int elem = b * 32 + e;
-    const v4i* Tb = reinterpret_cast<const v4i*>(T) + (size_t)b * TT * 64;
-    const int8_t* Tb8 = T + (size_t)b * TT * 64 * 16;
+    // shared_t: every wave reads batch 0's T (compute-bound timing: T stays in L1/L2)
+    const int tb = shared_t ? 0 : b;
+    const v4i* Tb = reinterpret_cast<const v4i*>(T) + (size_t)tb * TT * 64;
+    const int8_t* Tb8 = T + (size_t)tb * TT * 64 * 16;
     int* Ub = U + (size_t)b * QT * 16 * 64;
     for (int rep = 0; rep < reps; ++rep) {
       const v4i* Tr = Tb;
@@ -150,8 +152,8 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 }
 
 extern "C" int redc7_launch(const void* Afrag, const void* T, void* U, int nelem, int reps, int grid, void* dbg,
-                            void* stream) {
+                            int shared_t, void* stream) {
   hipLaunchKernelGGL(k_redc7, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const v4i*)Afrag, (const int8_t*)T,
-                     (int*)U, nelem, reps, (int*)dbg);
+                     (int*)U, nelem, reps, (int*)dbg, shared_t);
   return (int)hipGetLastError();
 }

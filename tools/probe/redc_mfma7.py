@@ -71,10 +71,11 @@ def main():
     U = torch.zeros(nelem * QT * 32, dtype=torch.int32, device=dev)
     dbg = torch.zeros(nelem * D, dtype=torch.int32, device=dev)
     lib = ctypes.CDLL(os.path.join(HERE, os.environ.get("REDC_LIB", "libredc_mfma7.so")))
-    lib.redc7_launch.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int] * 3 + [ctypes.c_void_p] * 2
+    lib.redc7_launch.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int] * 3 + [ctypes.c_void_p, ctypes.c_int,
+                                                                             ctypes.c_void_p]
     grid = max(1, nelem // 32 // 4)
     stream = torch.cuda.current_stream().cuda_stream
-    assert lib.redc7_launch(A.data_ptr(), T.data_ptr(), U.data_ptr(), nelem, 1, grid, dbg.data_ptr(), stream) == 0
+    assert lib.redc7_launch(A.data_ptr(), T.data_ptr(), U.data_ptr(), nelem, 1, grid, dbg.data_ptr(), 0, stream) == 0
     torch.cuda.synchronize()
     Qh = dbg[: nchk * D].view(nchk, D).cpu().numpy().astype(np.int64)
     Ub = U[: nchk * QT * 32].view(nchk // 32, QT, 16, 2, 32).cpu().numpy().astype(np.int64)
@@ -94,17 +95,19 @@ def main():
         s = t + q * N
         if s % R or value(Uh[i]) != s // R:
             ubad += 1
+    shared = int(os.environ.get("REDC_SHARED_T", "0"))
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    lib.redc7_launch(A.data_ptr(), T.data_ptr(), U.data_ptr(), nelem, reps, grid, None, stream)
+    lib.redc7_launch(A.data_ptr(), T.data_ptr(), U.data_ptr(), nelem, reps, grid, None, shared, stream)
     e0.record()
-    assert lib.redc7_launch(A.data_ptr(), T.data_ptr(), U.data_ptr(), nelem, reps, grid, None, stream) == 0
+    assert lib.redc7_launch(A.data_ptr(), T.data_ptr(), U.data_ptr(), nelem, reps, grid, None, shared, stream) == 0
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1)
     per = ms / 1e3 / (nelem * reps)
     print(json.dumps({"q_congruent": qbad == 0, "U_exact": ubad == 0, "max_q_digit": maxdig, "nelem": nelem,
                       "reps": reps, "ms": round(ms, 3), "ns_per_redc_elem": round(per * 1e9, 4),
-                      "simd_cycles_per_elem_at_2.3GHz": round(per * 2.3e9 * 1024, 1), "mfma_per_32_elems": 380}))
+                      "simd_cycles_per_elem_at_2.3GHz": round(per * 2.3e9 * 1024, 1), "mfma_per_32_elems": 380,
+                      "shared_t": shared}))
 
 
 if __name__ == "__main__":
