@@ -34,9 +34,12 @@ using namespace fphe::r28;
 typedef int v4i __attribute__((ext_vector_type(4)));
 
 constexpr int kT = 4, kE = 16, kNL = 148;
-constexpr int kRows = 160;               // slot rows per wave (K-tile 9 reads rows up to 159)
-constexpr int kJunk = 41 * 16;           // per-wave sink for the rows' T_low stores of lanes q != 0
-constexpr int kWave = kRows * 16 + kJunk;
+constexpr int kRows = 148;               // slot rows per wave
+constexpr int kWave = kRows * 16;
+#ifndef SQ_BLOCK_WAVES
+#define SQ_BLOCK_WAVES 6
+#endif
+constexpr int kBW = SQ_BLOCK_WAVES;      // waves per block (6: two blocks of LDS fit a CU at 3 waves/SIMD)
 constexpr int kW1 = 640, kW1Off = 48;    // W1[b + 48], b in [-48, 591]: bytes N'[b - j]
 constexpr int kW2 = 668, kW2Off = 12;    // W2[b + 12], b in [-12, 655]: bytes N[b - 16(j>>2) - (j&3)]
 static_assert(LL == 37 && LB == 28, "the digit layout assumes 28-bit limbs, 37 per lane");
@@ -44,14 +47,27 @@ static_assert(LL == 37 && LB == 28, "the digit layout assumes 28-bit limbs, 37 p
 __device__ __forceinline__ u32 spread7(u32 L) {  // 28-bit limb -> its four 7-bit digits as bytes
   return (L & 0x7Fu) | ((L << 1) & 0x7F00u) | ((L << 2) & 0x7F0000u) | ((L << 3) & 0x7F000000u);
 }
-__device__ __forceinline__ int from_below16(int x) {  // value of lane (l - 16) mod 64
+// value of lane (l - 16) mod 64, i.e. row g <- row g-1 of the wave, from two lane swaps
+// (VALU, no LDS round trip): permlane16_swap(x, x) = {[x0,x0,x2,x2], [x1,x1,x3,x3]} by rows,
+// permlane32_swap of the second = {[x1,x1,x1,x1], [x3,x3,x3,x3]}.
+#ifndef SQ_PERMLANE
+#define SQ_PERMLANE 1
+#endif
+__device__ __forceinline__ int from_below16(int x) {
+#if SQ_PERMLANE
+  const int g = (int)((threadIdx.x >> 4) & 3u);
+  const auto p16 = __builtin_amdgcn_permlane16_swap((unsigned)x, (unsigned)x, false, false);
+  const auto p32 = __builtin_amdgcn_permlane32_swap(p16[1], p16[1], false, false);
+  return (g & 1) ? (int)p16[0] : (g == 2 ? (int)p32[0] : (int)p32[1]);
+#else
   return __builtin_amdgcn_ds_bpermute((int)(((threadIdx.x - 16u) & 63u) << 2), x);
+#endif
 }
 
 // ---- phase A: squaring rows without reduction ---------------------------------------------
 template <int a>
-__device__ __forceinline__ void sqz_rows(u64 (&T)[LL], const L27& A, u32& b, const u32* bs, const u32* bnext,
-                                         u32* ws, u32 shf, u32 mkf, u32 mkx) {
+__device__ __forceinline__ void sqz_rows(u64 (&T)[LL], const L27& A, u32& b, u32* bs, const u32* bnext,
+                                         u32 shf, u32 mkf, u32 mkx) {
   // the slot holds 2a (fused-path convention): bf = 2a (q > s), a (q == s) or 0 (q < s)
   const u32 bf = __builtin_amdgcn_ubfe(b, shf, mkf);
   r27_sqrow<a>(T, A, bf, b, 0u);
@@ -62,11 +78,13 @@ __device__ __forceinline__ void sqz_rows(u64 (&T)[LL], const L27& A, u32& b, con
 #pragma unroll
   for (int j = 0; j < LL - 1; ++j) T[j] = T[j + 1];
   T[0] += X >> LB;
-  T[LL - 1] = (u64)dpp_from_next((u32)X & mkx);  // lane 0 sends 0: nothing crosses elements
-  ws[a * kE] = (u32)X & MASK;  // lane 0: limb 37s + a of T_low into its consumed slot; others: junk
+  T[LL - 1] = (u64)(dpp_from_next((u32)X) & mkx);  // the top lane (q = 3) takes 0: nothing crosses elements
+  // limb 37s + a of T_low (lane 0's X) into the slot the row consumed: broadcast over the
+  // element's 4 lanes, which then all store the same word
+  bs[a * kE] = dpp_bcast<kT>((u32)X) & MASK;
   asm volatile("" : "+v"(bn));
   b = bn;
-  if constexpr (a + 1 < LL) sqz_rows<a + 1>(T, A, b, bs, bnext, ws, shf, mkf, mkx);
+  if constexpr (a + 1 < LL) sqz_rows<a + 1>(T, A, b, bs, bnext, shf, mkf, mkx);
 }
 
 // ---- phase B helpers ------------------------------------------------------------------------
@@ -97,7 +115,7 @@ __device__ __forceinline__ u32 q_digits(const v4i& acc, int& prev0, int& prev1, 
 }
 
 template <int SKIP>
-__device__ __forceinline__ void mfma_sqr(L27& A, u32* bcol, u32 qoff, u32* wb, u32* junk, const v4i* W1s,
+__device__ __forceinline__ void mfma_sqr(L27& A, u32* bcol, u32 qoff, u32* wb, const v4i* W1s,
                                          const v4i* W2s, const u32* Nq, int q) {
   // phase A
 #pragma unroll
@@ -107,15 +125,14 @@ __device__ __forceinline__ void mfma_sqr(L27& A, u32* bcol, u32 qoff, u32* wb, u
   for (int j = 0; j < LL; ++j) T[j] = 0;
   {
     u32 b = bcol[0];
-    const u32 mkx = q == 0 ? 0u : MASK;
+    const u32 mkx = q == kT - 1 ? 0u : MASK;
 #pragma unroll 1
     for (int s = 0; s < (SKIP == 1 ? 0 : kT); ++s) {
       const u32 shf = q == s ? 1u : 0u;
       const u32 mkf = q > s ? 31u : (q == s ? 30u : 0u);
       u32* bs = bcol + s * LL * kE;
       const u32* bnext = s + 1 < kT ? bs + LL * kE : bcol;
-      u32* ws = q == 0 ? bs : junk;
-      sqz_rows<0>(T, A, b, bs, bnext, ws, shf, mkf, mkx);
+      sqz_rows<0>(T, A, b, bs, bnext, shf, mkf, mkx);
     }
   }
   L27 H;  // T_high as almost-normalised limbs (< 2^4050: no carry leaves the top lane)
@@ -128,12 +145,17 @@ __device__ __forceinline__ void mfma_sqr(L27& A, u32* bcol, u32 qoff, u32* wb, u
   for (int kt = 0; kt < 10; ++kt) {
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
-      const int row = 16 * kt + 4 * g + w;
+      int row = 16 * kt + 4 * g + w;
+      if (kt == 9) row = g == 0 ? row : 0;  // rows 148..159 are zero digits
       u32 L = wb[row * kE + c16];
-      if (kt == 9) L = row < kNL ? L : 0u;
+      if (kt == 9) L = g == 0 ? L : 0u;
       tf[kt][w] = (int)spread7(L);
     }
   }
+  // T_high -> the slot rows (after the reads above: one wave, LDS in order); product 2 adds
+  // its limbs to them, so no T_high registers stay live across the MFMA phase
+#pragma unroll
+  for (int j = 0; j < LL; ++j) bcol[qoff + j * kE] = H[j];
   const int w1l = kW1Off + c16 - 16 * g;
   v4i qv[10];  // q as B fragments: K-tile kt = output tiles 4kt..4kt+3 (37..39 zero)
   qv[9] = v4i{0, 0, 0, 0};
@@ -192,7 +214,8 @@ __device__ __forceinline__ void mfma_sqr(L27& A, u32* bcol, u32 qoff, u32* wb, u
       int val = lo + hin;
       if (t == 37 && g == 0) val += cval;
       if (t == 73 && g == 3) val += hi << LB;  // limb 148's carry, as 2^28 units of limb 147
-      wb[(4 * (t - 37) + g) * kE + c16] = (u32)val;
+      u32* rp = wb + (4 * (t - 37) + g) * kE + c16;
+      *rp = *rp + (u32)val;
     }
   }
   }
@@ -201,7 +224,7 @@ __device__ __forceinline__ void mfma_sqr(L27& A, u32* bcol, u32 qoff, u32* wb, u
   for (int j = 0; j < LL; ++j) {
     const int sv = (int)bcol[qoff + j * kE];
     const u32 bias = (j == 0 && q == 0) ? (1u << LB) : ((1u << LB) - 1u);
-    T[j] = (u64)H[j] + (u64)(long long)sv + (u64)Nq[j] + (u64)bias;
+    T[j] = (u64)(long long)sv + (u64)Nq[j] + (u64)bias;  // sv = T_high limb + P_high part
   }
   normalize_almost<kT>(T, A, q);
 }
@@ -212,12 +235,12 @@ __device__ __forceinline__ void mfma_sqr(L27& A, u32* bcol, u32 qoff, u32* wb, u
 #ifndef SQ_WAVES
 #define SQ_WAVES 2
 #endif
-template <int V>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(V >= 1 ? SQ_WAVES : 3))) void k_sqchain(const u32* __restrict__ X, u32* __restrict__ Y,
+template <int V, int BW = (V == 0 ? 4 : kBW)>
+__global__ __launch_bounds__(64 * BW) __attribute__((amdgpu_waves_per_eu(V >= 1 ? SQ_WAVES : 3))) void k_sqchain(const u32* __restrict__ X, u32* __restrict__ Y,
                                                  const u32* __restrict__ Nl, u32 np, const v4i* __restrict__ W,
                                                  int nelem, int S) {
   extern __shared__ __attribute__((aligned(16))) u32 lds[];
-  v4i* Ws = reinterpret_cast<v4i*>(lds + 4 * kWave);
+  v4i* Ws = reinterpret_cast<v4i*>(lds + BW * kWave);
   u32* Ns = reinterpret_cast<u32*>(Ws + kW1 + kW2);
   if (V >= 1) {
     for (int i = threadIdx.x; i < kW1 + kW2; i += blockDim.x) Ws[i] = W[i];
@@ -225,11 +248,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(V >= 1 ? SQ
     __syncthreads();
   }
   const int wib = (int)(threadIdx.x >> 6);
-  const int wave = (int)(blockIdx.x * 4 + wib);
+  const int wave = (int)(blockIdx.x * BW + wib);
   if (wave * kE >= nelem) return;
   Geo<kT> geo;
   u32* wb = lds + wib * kWave;
-  u32* junk = wb + kRows * kE + (threadIdx.x & 63u);
   u32* bcol = wb + geo.e;
   const u32 qoff = lds_qoff<kT>(geo.q);
   Mod<kT> N;
@@ -241,29 +263,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(V >= 1 ? SQ
 #pragma unroll 1
   for (int s = 0; s < S; ++s) {
     if constexpr (V == 0) sqr<kT>(A, bcol, qoff, N, np, geo.q);
-    else mfma_sqr<V - 1>(A, bcol, qoff, wb, junk, Ws, Ws + kW1, Ns + LL * geo.q, geo.q);
+    else mfma_sqr<V - 1>(A, bcol, qoff, wb, Ws, Ws + kW1, Ns + LL * geo.q, geo.q);
   }
   u32* y = Y + (size_t)(wave * kE + geo.e) * kNL + LL * geo.q;
 #pragma unroll
   for (int j = 0; j < LL; ++j) y[j] = A[j];
 }
 
+template <int V>
+static void launch(const void* X, void* Y, const void* Nl, unsigned np, const void* W, int nelem, int S,
+                   hipStream_t stream) {
+  constexpr int BW = V == 0 ? 4 : kBW;
+  const int waves = nelem / kE;
+  const int blocks = (waves + BW - 1) / BW;
+  const size_t lds = (size_t)BW * kWave * 4 + (V ? (size_t)(kW1 + kW2) * 16 + kNL * 4 : 0);
+  hipLaunchKernelGGL((k_sqchain<V>), dim3(blocks), dim3(64 * BW), lds, stream, (const u32*)X, (u32*)Y,
+                     (const u32*)Nl, np, (const v4i*)W, nelem, S);
+}
+
 extern "C" int sqchain_launch(int variant, const void* X, void* Y, const void* Nl, unsigned np, const void* W,
                               int nelem, int S, void* stream) {
-  const int waves = nelem / kE;
-  const int blocks = (waves + 3) / 4;
-  const size_t lds = (size_t)4 * kWave * 4 + (variant ? (size_t)(kW1 + kW2) * 16 + kNL * 4 : 0);
-  if (variant == 0)
-    hipLaunchKernelGGL(k_sqchain<0>, dim3(blocks), dim3(256), lds, (hipStream_t)stream, (const u32*)X, (u32*)Y,
-                       (const u32*)Nl, np, (const v4i*)W, nelem, S);
-  else if (variant == 2)
-    hipLaunchKernelGGL(k_sqchain<2>, dim3(blocks), dim3(256), lds, (hipStream_t)stream, (const u32*)X, (u32*)Y,
-                       (const u32*)Nl, np, (const v4i*)W, nelem, S);
-  else if (variant == 3)
-    hipLaunchKernelGGL(k_sqchain<3>, dim3(blocks), dim3(256), lds, (hipStream_t)stream, (const u32*)X, (u32*)Y,
-                       (const u32*)Nl, np, (const v4i*)W, nelem, S);
-  else
-    hipLaunchKernelGGL(k_sqchain<1>, dim3(blocks), dim3(256), lds, (hipStream_t)stream, (const u32*)X, (u32*)Y,
-                       (const u32*)Nl, np, (const v4i*)W, nelem, S);
+  hipStream_t st = (hipStream_t)stream;
+  if (variant == 0) launch<0>(X, Y, Nl, np, W, nelem, S, st);
+  else if (variant == 1) launch<1>(X, Y, Nl, np, W, nelem, S, st);
+  else if (variant == 2) launch<2>(X, Y, Nl, np, W, nelem, S, st);
+  else launch<3>(X, Y, Nl, np, W, nelem, S, st);
   return (int)hipGetLastError();
 }
