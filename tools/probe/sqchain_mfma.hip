@@ -50,6 +50,18 @@ __device__ __forceinline__ u32 spread7(u32 L) {  // 28-bit limb -> its four 7-bi
 // value of lane (l - 16) mod 64, i.e. row g <- row g-1 of the wave, from two lane swaps
 // (VALU, no LDS round trip): permlane16_swap(x, x) = {[x0,x0,x2,x2], [x1,x1,x3,x3]} by rows,
 // permlane32_swap of the second = {[x1,x1,x1,x1], [x3,x3,x3,x3]}.
+#ifndef SQ_STAMPS
+#define SQ_STAMPS 0
+#endif
+#if SQ_STAMPS
+__device__ unsigned long long g_stamp[8];
+#define STAMP(k) do { const unsigned long long _t = __builtin_amdgcn_s_memtime(); st[k] += _t - st_last; st_last = _t; } while (0)
+#else
+#define STAMP(k) do {} while (0)
+#endif
+#ifndef SQ_SPLIT_ACC
+#define SQ_SPLIT_ACC 1
+#endif
 #ifndef SQ_PERMLANE
 #define SQ_PERMLANE 1
 #endif
@@ -88,14 +100,34 @@ __device__ __forceinline__ void sqz_rows(u64 (&T)[LL], const L27& A, u32& b, u32
 }
 
 // ---- phase B helpers ------------------------------------------------------------------------
-// q digits from a C-layout tile (lane group g: positions 4g + r, r = 0..3; column sums of
-// unsigned 7-bit digits, < 592 * 127^2 < 2^23.2): positions are paired into 14-bit "wide"
-// digits w0 = v0 + 2^7 v1, w1 = v2 + 2^7 v3 (< 2^30.2), and two PARALLEL carry-save steps in
-// base 2^14 (every wide digit keeps its balanced 14-bit part and adds the carry of the wide
-// digit below: |carry| <= 75k, then <= 5) leave |w| <= 2^13 + 5, which splits into balanced
-// 7-bit digits within [-65, 64].  prev0/prev1: the carry of the previous tile's top wide
-// digit per step (valid in lane group 0).
+// q digits from a C-layout tile (lane group g: positions 4g + r, r = 0..3, i.e. one 28-bit
+// limb position; column sums of unsigned 7-bit digits, < 592 * 127^2 < 2^23.2).  The lane's
+// four sums form v = sum acc_r 2^(7r) (|v| < 2^44.3); ONE parallel carry-save step in base
+// 2^28 (keep the balanced low 28 bits, add the carry of the limb below, |carry| < 2^16.3)
+// leaves |x| <= 2^27 + 2^16.3, whose balanced 7-bit digits lie in [-64, 63] except the top
+// one, in [-65, 64].  prev: the previous tile's top-limb carry (valid in lane group 0).
+#ifndef SQ_QSTEP28
+#define SQ_QSTEP28 1
+#endif
 __device__ __forceinline__ u32 q_digits(const v4i& acc, int& prev0, int& prev1, int g) {
+#if SQ_QSTEP28
+  (void)prev1;
+  const int w0 = acc[0] + (acc[1] << 7), w1 = acc[2] + (acc[3] << 7);
+  const long long v = (long long)w1 * 16384 + (long long)w0;
+  const int c = (int)((v + (1ll << 27)) >> 28);
+  const int d = (int)((u32)v - ((u32)c << 28));
+  const int rot = from_below16(c);
+  const int cin = g > 0 ? rot : prev0;
+  prev0 = rot;
+  const int x = d + cin;
+  const int d0 = __builtin_amdgcn_sbfe(x, 0, 7);
+  const int x1 = (x - d0) >> 7;
+  const int d1 = __builtin_amdgcn_sbfe(x1, 0, 7);
+  const int x2 = (x1 - d1) >> 7;
+  const int d2 = __builtin_amdgcn_sbfe(x2, 0, 7);
+  const int d3 = (x2 - d2) >> 7;
+  return (u32)(d0 & 255) | ((u32)(d1 & 255) << 8) | ((u32)(d2 & 255) << 16) | ((u32)d3 << 24);
+#else
   int w0 = acc[0] + (acc[1] << 7);
   int w1 = acc[2] + (acc[3] << 7);
 #pragma unroll
@@ -112,11 +144,15 @@ __device__ __forceinline__ u32 q_digits(const v4i& acc, int& prev0, int& prev1, 
   const int l0 = __builtin_amdgcn_sbfe(w0, 0, 7), l1 = __builtin_amdgcn_sbfe(w1, 0, 7);
   const int h0 = (w0 - l0) >> 7, h1 = (w1 - l1) >> 7;
   return (u32)(l0 & 255) | ((u32)(h0 & 255) << 8) | ((u32)(l1 & 255) << 16) | ((u32)h1 << 24);
+#endif
 }
 
 template <int SKIP>
 __device__ __forceinline__ void mfma_sqr(L27& A, u32* bcol, u32 qoff, u32* wb, const v4i* W1s,
-                                         const v4i* W2s, const u32* Nq, int q) {
+                                         const v4i* W2s, const u32* Nq, int q, unsigned long long* st,
+                                         unsigned long long& st_last) {
+  (void)st;
+  (void)st_last;
   // phase A
 #pragma unroll
   for (int j = 0; j < LL; ++j) bcol[qoff + j * kE] = A[j] << 1;
@@ -135,6 +171,7 @@ __device__ __forceinline__ void mfma_sqr(L27& A, u32* bcol, u32 qoff, u32* wb, c
       sqz_rows<0>(T, A, b, bs, bnext, shf, mkf, mkx);
     }
   }
+  STAMP(0);
   L27 H;  // T_high as almost-normalised limbs (< 2^4050: no carry leaves the top lane)
   normalize_almost<kT>(T, H, q);
   // phase B
@@ -156,35 +193,60 @@ __device__ __forceinline__ void mfma_sqr(L27& A, u32* bcol, u32 qoff, u32* wb, c
   // its limbs to them, so no T_high registers stay live across the MFMA phase
 #pragma unroll
   for (int j = 0; j < LL; ++j) bcol[qoff + j * kE] = H[j];
+  STAMP(1);
   const int w1l = kW1Off + c16 - 16 * g;
   v4i qv[10];  // q as B fragments: K-tile kt = output tiles 4kt..4kt+3 (37..39 zero)
   qv[9] = v4i{0, 0, 0, 0};
   int pr0 = 0, pr1 = 0;
+  // software-pipelined: the MFMAs of tile m+1 are issued before the digit VALU work of tile m
+  auto chain1 = [&](int m) {
+    // two independent accumulators (even / odd K-tiles) so dependent MFMAs do not wait on
+    // each other back to back
+    v4i acc = {0, 0, 0, 0}, acc2 = {0, 0, 0, 0};
+#pragma unroll
+    for (int kt = 0; kt <= m / 4; ++kt) {
+      if (SQ_SPLIT_ACC && (kt & 1))
+        acc2 = __builtin_amdgcn_mfma_i32_16x16x64_i8(W1s[16 * (m - 4 * kt) + w1l], tf[kt], acc2, 0, 0, 0);
+      else
+        acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(W1s[16 * (m - 4 * kt) + w1l], tf[kt], acc, 0, 0, 0);
+    }
+    return SQ_SPLIT_ACC ? acc + acc2 : acc;
+  };
+  v4i cur = chain1(0);
 #pragma unroll
   for (int m = 0; m < 37; ++m) {
-#if SQ_TILE_BARRIER
     __builtin_amdgcn_sched_barrier(0);
-#endif
-    v4i acc = {0, 0, 0, 0};
-#pragma unroll
-    for (int kt = 0; kt <= m / 4; ++kt)
-      acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(W1s[16 * (m - 4 * kt) + w1l], tf[kt], acc, 0, 0, 0);
-    qv[m / 4][m % 4] = (int)q_digits(acc, pr0, pr1, g);
+    v4i nxt = {0, 0, 0, 0};
+    if (m + 1 < 37) nxt = chain1(m + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    qv[m / 4][m % 4] = (int)q_digits(cur, pr0, pr1, g);
+    cur = nxt;
   }
+  STAMP(2);
   const int w2l = kW2Off + c16 - 4 * g;
   int cval = 0, phi = 0;
-#pragma unroll
-  for (int t = 36; t < 74; ++t) {
-#if SQ_TILE_BARRIER
-    __builtin_amdgcn_sched_barrier(0);
-#endif
-    v4i acc = {0, 0, 0, 0};
+  auto chain2 = [&](int t) {
+    v4i acc = {0, 0, 0, 0}, acc2 = {0, 0, 0, 0};
     const int k0 = t > 40 ? (t - 40 + 3) / 4 : 0;
     const int k1 = t / 4 < 9 ? t / 4 : 9;
 #pragma unroll
     for (int kt = k0; kt <= k1; ++kt) {
-      acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(W2s[16 * (t - 4 * kt) + w2l], qv[kt], acc, 0, 0, 0);
+      if (SQ_SPLIT_ACC && ((kt - k0) & 1))
+        acc2 = __builtin_amdgcn_mfma_i32_16x16x64_i8(W2s[16 * (t - 4 * kt) + w2l], qv[kt], acc2, 0, 0, 0);
+      else
+        acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(W2s[16 * (t - 4 * kt) + w2l], qv[kt], acc, 0, 0, 0);
     }
+    return SQ_SPLIT_ACC ? acc + acc2 : acc;
+  };
+  v4i cur2 = chain2(36);
+#pragma unroll
+  for (int t = 36; t < 74; ++t) {
+    __builtin_amdgcn_sched_barrier(0);
+    v4i nxt = {0, 0, 0, 0};
+    if (t + 1 < 74) nxt = chain2(t + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    const v4i acc = cur2;
+    cur2 = nxt;
     if (t == 36) {
       // (T_low + P_low) / R from positions 576..591: this lane's rows 576 + 4g + r, plus the
       // T digits of limbs 144..147 (K-tile 9, group 0)
@@ -219,6 +281,7 @@ __device__ __forceinline__ void mfma_sqr(L27& A, u32* bcol, u32 qoff, u32* wb, c
     }
   }
   }
+  STAMP(3);
   // phase C
 #pragma unroll
   for (int j = 0; j < LL; ++j) {
@@ -227,6 +290,7 @@ __device__ __forceinline__ void mfma_sqr(L27& A, u32* bcol, u32 qoff, u32* wb, c
     T[j] = (u64)(long long)sv + (u64)Nq[j] + (u64)bias;  // sv = T_high limb + P_high part
   }
   normalize_almost<kT>(T, A, q);
+  STAMP(4);
 }
 
 #ifndef SQ_TILE_BARRIER
@@ -260,11 +324,17 @@ __global__ __launch_bounds__(64 * BW) __attribute__((amdgpu_waves_per_eu(V >= 1 
   L27 A;
 #pragma unroll
   for (int k = 0; k < LP; ++k) A.set2(k, x[2 * k], 2 * k + 1 < LL ? x[2 * k + 1] : 0u);
+  unsigned long long st[5] = {0, 0, 0, 0, 0};
+  unsigned long long st_last = SQ_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
 #pragma unroll 1
   for (int s = 0; s < S; ++s) {
     if constexpr (V == 0) sqr<kT>(A, bcol, qoff, N, np, geo.q);
-    else mfma_sqr<V - 1>(A, bcol, qoff, wb, Ws, Ws + kW1, Ns + LL * geo.q, geo.q);
+    else mfma_sqr<V - 1>(A, bcol, qoff, wb, Ws, Ws + kW1, Ns + LL * geo.q, geo.q, st, st_last);
   }
+#if SQ_STAMPS
+  if (V >= 1 && (threadIdx.x & 63) == 0)
+    for (int k = 0; k < 5; ++k) atomicAdd(&g_stamp[k], st[k]);
+#endif
   u32* y = Y + (size_t)(wave * kE + geo.e) * kNL + LL * geo.q;
 #pragma unroll
   for (int j = 0; j < LL; ++j) y[j] = A[j];
@@ -289,4 +359,13 @@ extern "C" int sqchain_launch(int variant, const void* X, void* Y, const void* N
   else if (variant == 2) launch<2>(X, Y, Nl, np, W, nelem, S, st);
   else launch<3>(X, Y, Nl, np, W, nelem, S, st);
   return (int)hipGetLastError();
+}
+
+extern "C" int sqchain_stamps(unsigned long long* out) {
+#if SQ_STAMPS
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamp), sizeof(unsigned long long) * 5);
+#else
+  (void)out;
+  return -1;
+#endif
 }

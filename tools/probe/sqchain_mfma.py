@@ -99,6 +99,12 @@ def main():
         ms = e0.elapsed_time(e1)
         out[f"v{variant}_ms"] = round(ms, 3)
         out[f"v{variant}_ns_per_sqr"] = round(ms * 1e6 / (nelem * S), 4)
+    st = (ctypes.c_ulonglong * 5)()
+    if lib.sqchain_stamps(st) == 0:
+        # totals over every wave of every launch of variant 1 (checks + warm-up + timed)
+        tot = sum(st)
+        out["phase_share"] = {k: round(st[i] / tot, 3) for i, k in
+                              enumerate(["A_rows", "tfrag_Hstore", "product1_q", "product2_U", "phaseC"])}
     if "v0_ms" in out and "v1_ms" in out:
         out["speedup_mfma"] = round(out["v0_ms"] / out["v1_ms"], 3)
     print(json.dumps(out))
