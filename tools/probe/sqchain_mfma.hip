@@ -50,6 +50,9 @@ __device__ __forceinline__ u32 spread7(u32 L) {  // 28-bit limb -> its four 7-bi
 // value of lane (l - 16) mod 64, i.e. row g <- row g-1 of the wave, from two lane swaps
 // (VALU, no LDS round trip): permlane16_swap(x, x) = {[x0,x0,x2,x2], [x1,x1,x3,x3]} by rows,
 // permlane32_swap of the second = {[x1,x1,x1,x1], [x3,x3,x3,x3]}.
+#ifndef SQ_STAGGER
+#define SQ_STAGGER 0
+#endif
 #ifndef SQ_STAMPS
 #define SQ_STAMPS 0
 #endif
@@ -324,6 +327,14 @@ __global__ __launch_bounds__(64 * BW) __attribute__((amdgpu_waves_per_eu(V >= 1 
   L27 A;
 #pragma unroll
   for (int k = 0; k < LP; ++k) A.set2(k, x[2 * k], 2 * k + 1 < LL ? x[2 * k + 1] : 0u);
+#if SQ_STAGGER
+  // waves sharing a SIMD (wib, wib + 4, wib + 8 of a 12-wave block) start a third of a
+  // squaring apart, so their product phases do not coincide
+  if (V == 1) {
+    const int lag = (int)(wib / 4);
+    for (int i = 0; i < lag * SQ_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
+  }
+#endif
   unsigned long long st[5] = {0, 0, 0, 0, 0};
   unsigned long long st_last = SQ_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
 #pragma unroll 1
