@@ -1,15 +1,12 @@
-// Device multi-precision Montgomery arithmetic for gfx950 (CDNA4).
+// Shared device helpers for gfx950 (CDNA4): buffer-descriptor tiles, the wave-uniform
+// 32-bit CIOS product the decrypt CRT tail uses for its one-off products mod p and q
+// (fate_phe.hip crt_tail / crt_combine), and small wave reductions.  The ciphertext
+// engine itself is the reduced-radix one (mont27_dev.h).
 //
-// Layout decisions:
-//  * one ciphertext element per lane; its L limbs of the running value live in VGPRs
-//    (A[L]) and the CIOS accumulator T[L+1] too, so the inner MAC loop has no
-//    cross-lane traffic at all;
-//  * the runtime-indexed operand (b_i in CIOS) is staged in LDS in a [limb][lane]
-//    slot, so lane l reads slot[i*64] -- 64 consecutive dwords per wave, conflict-free;
-//  * the modulus N and every shared exponent are identical for all elements of a key
-//    (wave-uniform), so they are read through uniform pointers -> SGPR scalar loads and
-//    v_mad_u64_u32 takes them as scalar operands; window digits of a shared exponent
-//    are uniform, so control flow never diverges in the modexp.
+// 32-bit CIOS layout: one element per lane; its L limbs live in VGPRs (A[L]) with the
+// accumulator T[L+1]; the runtime-indexed operand b_i is staged in an LDS [limb][lane]
+// slot (64 consecutive dwords per wave, conflict-free); the modulus is wave-uniform and
+// read through scalar loads.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -46,41 +43,16 @@ __device__ __forceinline__ Tile make_tile(const void* base, u32 bytes, int lane)
 // ---- LDS slot / tile helpers ----------------------------------------------------------
 // `slot` points at this lane's column of a [limb][64] LDS tile.
 template <int L>
-__device__ __forceinline__ void slot_store(u32* slot, const u32 (&A)[L]) {
-#pragma unroll
-  for (int j = 0; j < L; ++j) slot[j * FPHE_WAVE] = A[j];
-}
-
-template <int L>
 __device__ __forceinline__ void slot_store_uniform(u32* slot, const u32* __restrict__ src) {
 #pragma unroll
   for (int j = 0; j < L; ++j) slot[j * FPHE_WAVE] = src[j];
 }
 
-template <int L>
-__device__ __forceinline__ void slot_store_small(u32* slot, u32 v) {
-  slot[0] = v;
-#pragma unroll
-  for (int j = 1; j < L; ++j) slot[j * FPHE_WAVE] = 0u;
-}
-
 // entry-relative scalar byte offsets: limb j of entry k of an L-limb tile table
-template <int L>
-__device__ __forceinline__ void tile_store(const Tile& t, u32 soff, const u32 (&A)[L]) {
-#pragma unroll
-  for (int j = 0; j < L; ++j) t.st(A[j], soff + j * 256u);
-}
-
 template <int L>
 __device__ __forceinline__ void tile_load(u32 (&A)[L], const Tile& t, u32 soff) {
 #pragma unroll
   for (int j = 0; j < L; ++j) A[j] = t.ld(soff + j * 256u);
-}
-
-template <int L>
-__device__ __forceinline__ void tile_to_slot(u32* slot, const Tile& t, u32 soff) {
-#pragma unroll
-  for (int j = 0; j < L; ++j) slot[j * FPHE_WAVE] = t.ld(soff + j * 256u);
 }
 
 // ---- Montgomery multiplication (CIOS) ------------------------------------------------
@@ -148,51 +120,6 @@ __device__ __forceinline__ void mont_mul(u32 (&A)[L], const u32* slot,
   }
 }
 
-// A <- A^2 * R^-1 mod N  (stages A in the slot first)
-template <int L>
-__device__ __forceinline__ void mont_sqr(u32 (&A)[L], u32* slot, const u32* __restrict__ N, const u32 n0inv) {
-  slot_store<L>(slot, A);
-  mont_mul<L>(A, slot, N, n0inv);
-}
-
-// ---- fixed-window modexp with a wave-uniform exponent ---------------------------------
-// In : A = X (Montgomery form, < N).  Out: A = X^E (Montgomery form).
-// E  : uniform limbs, ebits = exact bit length (>= 1).
-// tb : the wave's global table of (1<<W) entries x L limbs (entry k at byte k*L*256).
-template <int L, int W>
-__device__ __forceinline__ void powm_uniform(u32 (&A)[L], u32* slot, const Tile& tb,
-                                             const u32* __restrict__ N, const u32 n0inv,
-                                             const u32* __restrict__ E, const int ebits) {
-  constexpr u32 TE = L * 256u;  // bytes per table entry (per wave)
-  slot_store<L>(slot, A);       // slot = X for the whole table build
-  tile_store<L>(tb, 1 * TE, A);
-#pragma unroll 1
-  for (int k = 2; k < (1 << W); ++k) {
-    mont_mul<L>(A, slot, N, n0inv);  // A = X^k
-    tile_store<L>(tb, (u32)k * TE, A);
-  }
-  const int nwin = (ebits + W - 1) / W;
-  auto digit = [&](int w) -> int {
-    const int b0 = w * W;
-    const int limb = b0 >> 5, off = b0 & 31;
-    u32 v = E[limb] >> off;
-    if (off + W > 32) v |= E[limb + 1] << (32 - off);  // exponent arrays carry a zero pad limb
-    return (int)(v & ((1u << W) - 1));
-  };
-  int d = digit(nwin - 1);
-  tile_load<L>(A, tb, (u32)d * TE);
-#pragma unroll 1
-  for (int w = nwin - 2; w >= 0; --w) {
-#pragma unroll 1
-    for (int s = 0; s < W; ++s) mont_sqr<L>(A, slot, N, n0inv);
-    d = digit(w);
-    if (d != 0) {
-      tile_to_slot<L>(slot, tb, (u32)d * TE);
-      mont_mul<L>(A, slot, N, n0inv);
-    }
-  }
-}
-
 // ---- small helpers ------------------------------------------------------------------
 __device__ __forceinline__ int wave_max_int(int v) {
 #pragma unroll
@@ -201,18 +128,6 @@ __device__ __forceinline__ int wave_max_int(int v) {
     v = o > v ? o : v;
   }
   return v;
-}
-
-// a >= b over L limbs (a per-lane regs, b uniform)
-template <int L>
-__device__ __forceinline__ bool geq_uniform(const u32 (&a)[L], const u32* __restrict__ b) {
-  u32 br = 0;
-#pragma unroll
-  for (int j = 0; j < L; ++j) {
-    const u64 d = (u64)a[j] - b[j] - br;
-    br = (u32)(d >> 63);
-  }
-  return br == 0;
 }
 
 }  // namespace fphe
