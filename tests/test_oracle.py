@@ -67,6 +67,41 @@ def test_fixtures_vs_gmp(gmp, bits):
         assert g.add_ct(a, b) == int(o, 16)
 
 
+@pytest.mark.parametrize("bits", [1024, 2048])
+def test_ops_fixtures_vs_gmp(gmp, bits):
+    """The ops fixtures' neg and ct x pt outputs are what libgmp computes: mpz_invert (powm by
+    -1) for neg, mpz_powm over every branch of Ciphertext::mul, a negative exponent meaning
+    an inverse first (fixedpoint_paillier/src/lib.rs:259-263, 334-349)."""
+    fx, sk, pk = keys(bits)
+    with open(os.path.join(HERE, "golden", f"paillier_{bits}_ops.json")) as f:
+        ops = json.load(f)
+    ns, mx = pk.ns, pk.max_int
+    for (a, ea), (o, eo) in zip(ops["neg"]["a"], ops["neg"]["out"]):
+        assert gmp.powm(int(a, 16), -1, ns) == int(o, 16) and eo == ea
+    kinds = set()
+    for (c, ec), (s, es), (o, eo), kind in zip(ops["mul"]["c"], ops["mul"]["p"], ops["mul"]["out"],
+                                               ops["mul"]["kind"]):
+        c, s = int(c, 16), int(s, 16)
+        if s >= pk.n - mx:  # encoded negative int: invert, then powm by n - s
+            want = gmp.powm(gmp.powm(c, -1, ns), pk.n - s, ns)
+            kinds.add("invert")
+        else:
+            assert s <= mx
+            want = gmp.powm(c, s, ns)
+            kinds.add("negative_exponent" if s < 0 else "powm")
+        assert want == int(o, 16) and eo == ec + es, kind
+    assert kinds == {"invert", "negative_exponent", "powm"}
+    # sub = add(a, neg(b)) and rsub = add(neg(a), b), re-derived with the oracle's add on
+    # the libgmp inverse
+    for (a, ea), (b, eb), (o, eo), (r, er) in zip(ops["sub"]["a"], ops["sub"]["b"], ops["sub"]["out"],
+                                                  ops["sub"]["rsub"]):
+        A, B = O.Ciphertext(int(a, 16), ea), O.Ciphertext(int(b, 16), eb)
+        nb = O.Ciphertext(gmp.powm(B.c, -1, ns), eb)
+        na = O.Ciphertext(gmp.powm(A.c, -1, ns), ea)
+        assert O.ct_add(pk, A, nb) == O.Ciphertext(int(o, 16), eo)
+        assert O.ct_add(pk, na, B) == O.Ciphertext(int(r, 16), er)
+
+
 def test_invert_branch_and_negative_significands(gmp):
     """encrypt's m > n/4 branch (invert) and negative m (negative ciphertext integer)."""
     fx, sk, pk = keys(1024)

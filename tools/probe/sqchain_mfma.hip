@@ -79,16 +79,27 @@ __device__ __forceinline__ int from_below16(int x) {
 #endif
 }
 
+#ifndef SQ_EARLY_B
+#define SQ_EARLY_B 1
+#endif
 // ---- phase A: squaring rows without reduction ---------------------------------------------
 template <int a>
 __device__ __forceinline__ void sqz_rows(u64 (&T)[LL], const L27& A, u32& b, u32* bs, const u32* bnext,
                                          u32 shf, u32 mkf, u32 mkx) {
   // the slot holds 2a (fused-path convention): bf = 2a (q > s), a (q == s) or 0 (q < s)
   const u32 bf = __builtin_amdgcn_ubfe(b, shf, mkf);
-  r27_sqrow<a>(T, A, bf, b, 0u);
+  // b_{i+1} is read before the row's MACs so its LDS latency hides under them (read after
+  // the row it was waited for ~8 instructions later, one exposed LDS latency per row)
   u32 bn;
+#if SQ_EARLY_B
   if constexpr (a + 1 < LL) bn = bs[(a + 1) * kE];
   else bn = bnext[0];
+  r27_sqrow<a>(T, A, bf, b, 0u);
+#else
+  r27_sqrow<a>(T, A, bf, b, 0u);
+  if constexpr (a + 1 < LL) bn = bs[(a + 1) * kE];
+  else bn = bnext[0];
+#endif
   const u64 X = T[0];
 #pragma unroll
   for (int j = 0; j < LL - 1; ++j) T[j] = T[j + 1];
@@ -147,6 +158,28 @@ __device__ __forceinline__ u32 q_digits(const v4i& acc, int& prev0, int& prev1, 
   const int l0 = __builtin_amdgcn_sbfe(w0, 0, 7), l1 = __builtin_amdgcn_sbfe(w1, 0, 7);
   const int h0 = (w0 - l0) >> 7, h1 = (w1 - l1) >> 7;
   return (u32)(l0 & 255) | ((u32)(h0 & 255) << 8) | ((u32)(l1 & 255) << 16) | ((u32)h1 << 24);
+#endif
+}
+
+// Scheduling of one product tile's table reads and MFMAs: with SQ_LOOKAHEAD = L > 0 the
+// first L ds_read_b128 are issued together and every MFMA is followed by the read L places
+// ahead, so an MFMA waits for a read issued L MFMAs (>= 16 L cycles) earlier instead of the
+// one issued just before it (the compiler's own schedule keeps one read in flight).
+#ifndef SQ_LOOKAHEAD
+#define SQ_LOOKAHEAD 0
+#endif
+__device__ __forceinline__ void lookahead_groups(int n) {
+#if SQ_LOOKAHEAD
+  constexpr int L = SQ_LOOKAHEAD;
+#pragma unroll
+  for (int i = 0; i < (n < L ? n : L); ++i) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+#pragma unroll
+  for (int i = 0; i < n; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    if (i + L < n) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+  }
+#else
+  (void)n;
 #endif
 }
 
@@ -213,6 +246,7 @@ __device__ __forceinline__ void mfma_sqr(L27& A, u32* bcol, u32 qoff, u32* wb, c
       else
         acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(W1s[16 * (m - 4 * kt) + w1l], tf[kt], acc, 0, 0, 0);
     }
+    lookahead_groups(m / 4 + 1);
     return SQ_SPLIT_ACC ? acc + acc2 : acc;
   };
   v4i cur = chain1(0);
@@ -239,6 +273,7 @@ __device__ __forceinline__ void mfma_sqr(L27& A, u32* bcol, u32 qoff, u32* wb, c
       else
         acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(W2s[16 * (t - 4 * kt) + w2l], qv[kt], acc, 0, 0, 0);
     }
+    lookahead_groups(k1 - k0 + 1);
     return SQ_SPLIT_ACC ? acc + acc2 : acc;
   };
   v4i cur2 = chain2(36);
@@ -296,6 +331,8 @@ __device__ __forceinline__ void mfma_sqr(L27& A, u32* bcol, u32 qoff, u32* wb, c
   STAMP(4);
 }
 
+__device__ int g_roles[16];
+extern "C" int sqchain_roles(int* out) { return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_roles), sizeof(int) * 16); }
 #ifndef SQ_TILE_BARRIER
 #define SQ_TILE_BARRIER 1
 #endif
@@ -315,6 +352,19 @@ __global__ __launch_bounds__(64 * BW) __attribute__((amdgpu_waves_per_eu(V >= 1 
     __syncthreads();
   }
   const int wib = (int)(threadIdx.x >> 6);
+  bool role_b = false;
+  if constexpr (V == 4) {
+    // SIMD of this wave from HW_ID bits 5:4 (gfx9 layout), then an arrival order per SIMD
+    __shared__ int simd_cnt[4];
+    if (threadIdx.x < 4) simd_cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const int simd = (__builtin_amdgcn_s_getreg(4 | (4 << 6) | (1 << 11))) & 3;
+    int k = 0;
+    if ((threadIdx.x & 63) == 0) k = atomicAdd(&simd_cnt[simd], 1);
+    k = __builtin_amdgcn_readfirstlane(k);
+    role_b = k == 0;
+    if ((threadIdx.x & 63) == 0 && blockIdx.x == 0) g_roles[wib] = simd * 16 + k;
+  }
   const int wave = (int)(blockIdx.x * BW + wib);
   if (wave * kE >= nelem) return;
   Geo<kT> geo;
@@ -340,7 +390,12 @@ __global__ __launch_bounds__(64 * BW) __attribute__((amdgpu_waves_per_eu(V >= 1 
 #pragma unroll 1
   for (int s = 0; s < S; ++s) {
     if constexpr (V == 0) sqr<kT>(A, bcol, qoff, N, np, geo.q);
-    else mfma_sqr<V - 1>(A, bcol, qoff, wb, Ws, Ws + kW1, Ns + LL * geo.q, geo.q, st, st_last);
+    else if constexpr (V == 4) {
+      // overlap test: the first wave to arrive on each SIMD runs only the product phase,
+      // the others only the rows: two row waves and one product wave per SIMD
+      if (role_b) mfma_sqr<1>(A, bcol, qoff, wb, Ws, Ws + kW1, Ns + LL * geo.q, geo.q, st, st_last);
+      else mfma_sqr<2>(A, bcol, qoff, wb, Ws, Ws + kW1, Ns + LL * geo.q, geo.q, st, st_last);
+    } else mfma_sqr<V - 1>(A, bcol, qoff, wb, Ws, Ws + kW1, Ns + LL * geo.q, geo.q, st, st_last);
   }
 #if SQ_STAMPS
   if (V >= 1 && (threadIdx.x & 63) == 0)
@@ -368,7 +423,8 @@ extern "C" int sqchain_launch(int variant, const void* X, void* Y, const void* N
   if (variant == 0) launch<0>(X, Y, Nl, np, W, nelem, S, st);
   else if (variant == 1) launch<1>(X, Y, Nl, np, W, nelem, S, st);
   else if (variant == 2) launch<2>(X, Y, Nl, np, W, nelem, S, st);
-  else launch<3>(X, Y, Nl, np, W, nelem, S, st);
+  else if (variant == 3) launch<3>(X, Y, Nl, np, W, nelem, S, st);
+  else launch<4>(X, Y, Nl, np, W, nelem, S, st);
   return (int)hipGetLastError();
 }
 

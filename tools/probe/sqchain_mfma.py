@@ -105,6 +105,10 @@ def main():
         tot = sum(st)
         out["phase_share"] = {k: round(st[i] / tot, 3) for i, k in
                               enumerate(["A_rows", "tfrag_Hstore", "product1_q", "product2_U", "phaseC"])}
+    if 4 in variants:
+        ro = (ctypes.c_int * 16)()
+        lib.sqchain_roles(ro)
+        out["v4_roles_simd_k"] = [(r >> 4, r & 15) for r in ro[:12]]
     if "v0_ms" in out and "v1_ms" in out:
         out["speedup_mfma"] = round(out["v0_ms"] / out["v1_ms"], 3)
     print(json.dumps(out))
