@@ -332,3 +332,58 @@ def test_extreme_operands(bits):
     for k in (pk, pk_pub):  # key-holder CRT path and public-key path
         enc = k.encrypt_encoded(P.PlaintextVector.from_ints(sigs, [0] * len(sigs)), True, r=rs)
         assert host(enc) == [(c.c, c.exp) for c in want]
+
+
+def _rows(v, idx):
+    """(signed integer, exp) of elements idx of a device vector, read without a full copy."""
+    idx_t = torch.as_tensor(idx, dtype=torch.long, device=v.C.device)
+    words = v.C[idx_t // 64, :, idx_t % 64].cpu().numpy().view(np.uint32)
+    mags = [sum(int(w) << (32 * k) for k, w in enumerate(row)) for row in words]
+    return mags, v.sign[idx_t].cpu().tolist(), v.exp[idx_t].cpu().tolist()
+
+
+def test_add_across_launch_chunks():
+    """ct-add over vectors larger than one fphe_add_ordered launch (paillier.ADD_CHUNK
+    elements, 2 GiB of ciphertext words at 2048 bits): the chunks' gap orders, tile offsets
+    and ragged last tile, checked element by element against the oracle at the chunk seams,
+    the ends and random positions (fixedpoint_paillier/src/lib.rs:301-333)."""
+    p, q, sk, pk, coder, osk, opk = load(2048)
+    n = P.ADD_CHUNK + 3 * 64 + 5
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(5)
+    L2 = pk._key.L2
+
+    def rand_vec():
+        v = P.CiphertextVector.empty(n, L2, dev)
+        v.C.copy_(torch.randint(-(1 << 31), 1 << 31, v.C.shape, generator=g, device=dev, dtype=torch.int32))
+        v.C[:, L2 - 1, :] = 0  # < 2^(32(L2-1)) < n^2: canonical residues
+        v.sign.copy_(torch.randint(0, 2, v.sign.shape, generator=g, device=dev, dtype=torch.uint8))
+        v.exp.copy_(torch.randint(-16, -11, v.exp.shape, generator=g, device=dev, dtype=torch.int32))
+        v.n = pk.n
+        return v
+
+    a, b = rand_vec(), rand_vec()
+    seam = P.ADD_CHUNK
+    lits = [0, seam - 1, seam, n - 1]
+    for i in lits[:2]:  # literal 1s on both sides of the seam
+        a.C[i // 64, :, i % 64] = 0
+        a.C[i // 64, 0, i % 64] = 1
+        a.sign[i] = 0
+    for i in lits[2:]:
+        b.C[i // 64, :, i % 64] = 0
+        b.C[i // 64, 0, i % 64] = 1
+        b.sign[i] = 0
+    out = a.add(pk, b)
+    rng = random.Random(9)
+    idx = sorted(set(lits + [1, 63, 64, seam - 64, seam - 2, seam + 1, seam + 63, seam + 64, n - 2, n - 64]
+                     + [rng.randrange(n) for _ in range(24)]))
+    ma, sa, ea = _rows(a, idx)
+    mb, sb, eb = _rows(b, idx)
+    mo, so, eo = _rows(out, idx)
+    ns = opk.ns
+    for k in range(len(idx)):
+        ca = O.Ciphertext(ma[k] - ns if sa[k] and ma[k] else ma[k], ea[k])
+        cb = O.Ciphertext(mb[k] - ns if sb[k] and mb[k] else mb[k], eb[k])
+        want = O.ct_add(opk, ca, cb)
+        got = mo[k] - ns if so[k] and mo[k] else mo[k]
+        assert (got, eo[k]) == (want.c, want.exp), idx[k]
