@@ -203,11 +203,14 @@ __global__ __launch_bounds__(256) void k_chacha_blocks(ChaChaKey ck, u32 counter
   }
 }
 
+// element e of the launch draws the stream of element ebase + e of the call (a call split
+// into spans draws exactly what one launch over all its elements would)
 template <int L1>
-__global__ __launch_bounds__(256) void k_draw_r(KeyArgs K, size_t count, ChaChaKey ck, u64 nonce, u32* __restrict__ R) {
+__global__ __launch_bounds__(256) void k_draw_r(KeyArgs K, size_t count, ChaChaKey ck, u64 nonce, size_t ebase,
+                                                 u32* __restrict__ R) {
   for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < count; e += (size_t)gridDim.x * blockDim.x) {
     u32 r[L1];
-    draw_r<L1>(r, K, ck, nonce, e);
+    draw_r<L1>(r, K, ck, nonce, ebase + e);
 #pragma unroll
     for (int j = 0; j < L1; ++j) R[tiled(e, L1, j)] = r[j];
   }
@@ -565,6 +568,21 @@ fphe_status ensure_scratch(fphe_ctx* c, size_t bytes, hipStream_t s) {
   return FPHE_OK;
 }
 
+// Long calls run as spans of whole grid rounds, at least kSpanTarget elements each (a
+// 2048-bit encrypt of 2^21 elements is ~6 s): no single launch of a 100M-element call runs
+// for minutes, the per-span scratch (drawn nonces, CRT halves) stays ~1 GB instead of
+// growing with the call, and every span but the last fills its grid's last round exactly.
+// FPHE_SPAN_TARGET overrides the target (tests force several spans on small calls).
+constexpr size_t kSpanTarget = (size_t)1 << 21;
+template <typename KernT>
+size_t span_elems(const fphe_ctx* c, KernT k, size_t lds, int E) {
+  const char* env = getenv("FPHE_SPAN_TARGET");
+  const size_t target = env ? (size_t)strtoull(env, nullptr, 10) : kSpanTarget;
+  const size_t cap = (size_t)occ_grid(c, k, lds, (size_t)1 << 40) * kWavesPerBlock * (size_t)E;  // one round
+  const size_t rounds = target / cap > 0 ? target / cap : 1;
+  return cap * rounds;  // a multiple of 64: spans start on tile boundaries
+}
+
 template <typename KernT>
 void set_lds(KernT k, size_t bytes) {
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
@@ -589,23 +607,30 @@ fphe_status launch_encrypt27(fphe_ctx* c, const uint32_t* P, uint32_t lp, const 
   auto kern = KS<TPI>::template encrypt<L, kWinSlide>();
   const size_t lds = (size_t)kWavesPerBlock * LDSW * E * 4;
   set_lds(kern, lds);
-  const unsigned grid = occ_grid(c, kern, lds, (count + E - 1) / E, "encrypt27");
+  const size_t span = span_elems(c, kern, lds, E);
+  const size_t m0 = count < span ? count : span;
+  const unsigned grid = occ_grid(c, kern, lds, (m0 + E - 1) / E, "encrypt27");
   const size_t tbytes = (size_t)grid * kWavesPerBlock * kTabEntries<kWinSlide> * rad_ll(TPI) * FPHE_WAVE * 4;
-  const size_t rbytes = (size_t)ntiles_of(count) * L1 * FPHE_WAVE * 4;
+  const size_t rbytes = (size_t)ntiles_of(m0) * L1 * FPHE_WAVE * 4;
   const bool draw = obf && !r;
   if (ensure_scratch(c, tbytes + (draw ? rbytes : 0), s) != FPHE_OK) return FPHE_ERR_HIP;
-  const u32* rbuf = r;
-  if (draw) {
-    u32* rdev = c->scratch + tbytes / 4;
-    ChaChaKey ck;
+  ChaChaKey ck;
+  if (draw)
     for (int i = 0; i < 8; ++i) ck.k[i] = key[i];
-    const unsigned rgrid = (unsigned)std::min<size_t>((count + 255) / 256, (size_t)c->cus * 4);
-    hipLaunchKernelGGL(k_draw_r<L1>, dim3(rgrid), dim3(256), 0, s, c->K, count, ck, nonce, rdev);
-    rbuf = rdev;
+  for (size_t e0 = 0; e0 < count; e0 += span) {  // spans run in stream order over one scratch
+    const size_t m = count - e0 < span ? count - e0 : span, t0 = e0 / FPHE_WAVE;
+    const u32* rbuf = r ? r + t0 * L1 * FPHE_WAVE : nullptr;
+    if (draw) {
+      u32* rdev = c->scratch + tbytes / 4;
+      const unsigned rgrid = (unsigned)std::min<size_t>((m + 255) / 256, (size_t)c->cus * 4);
+      hipLaunchKernelGGL(k_draw_r<L1>, dim3(rgrid), dim3(256), 0, s, c->K, m, ck, nonce, e0, rdev);
+      rbuf = rdev;
+    }
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, P + t0 * lp * FPHE_WAVE, lp, neg + e0, m, obf,
+                       rbuf, C + t0 * L * FPHE_WAVE, sign + e0, c->scratch, (u32)LDSW);
+    if (hipGetLastError() != hipSuccess) return FPHE_ERR_HIP;
   }
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, P, lp, neg, count, obf, rbuf, C, sign, c->scratch,
-                     (u32)LDSW);
-  return hip_ok(hipGetLastError());
+  return FPHE_OK;
 }
 
 template <int L>
@@ -614,18 +639,25 @@ fphe_status launch_decrypt27(fphe_ctx* c, const uint32_t* C, size_t count, uint3
   auto kern = KS<TPI>::template pow_half<L, kWinSlide, false>();
   const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
   set_lds(kern, lds);
-  const unsigned grid = occ_grid(c, kern, lds, (count + E - 1) / E, "decrypt_pow27");
+  const size_t span = span_elems(c, kern, lds, E);
+  const size_t m0 = count < span ? count : span;
+  const unsigned grid = occ_grid(c, kern, lds, (m0 + E - 1) / E, "decrypt_pow27");
   const size_t tbytes = (size_t)grid * kWavesPerBlock * kTabEntries<kWinSlide> * rad_ll(TPI) * FPHE_WAVE * 4;
-  const size_t ybytes = (size_t)ntiles_of(count) * 2 * LH * FPHE_WAVE * 4;
+  const size_t ybytes = (size_t)ntiles_of(m0) * 2 * LH * FPHE_WAVE * 4;
   if (ensure_scratch(c, tbytes + ybytes, s) != FPHE_OK) return FPHE_ERR_HIP;
   u32* Y = c->scratch + tbytes / 4;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, C, count, Y, c->scratch, (u32)NL);
   auto kcrt = k_decrypt_crt<L>;
   const size_t lds2 = (size_t)kWavesPerBlock * LQ * FPHE_WAVE * 4;
   set_lds(kcrt, lds2);
-  const unsigned grid2 = grid_for(c, count, bpc_for_slot(LQ));
-  hipLaunchKernelGGL(kcrt, dim3(grid2), dim3(kBlock), lds2, s, c->K, Y, ntiles_of(count), P);
-  return hip_ok(hipGetLastError());
+  for (size_t e0 = 0; e0 < count; e0 += span) {
+    const size_t m = count - e0 < span ? count - e0 : span, t0 = e0 / FPHE_WAVE;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, C + t0 * L * FPHE_WAVE, m, Y, c->scratch,
+                       (u32)NL);
+    const unsigned grid2 = grid_for(c, m, bpc_for_slot(LQ));
+    hipLaunchKernelGGL(kcrt, dim3(grid2), dim3(kBlock), lds2, s, c->K, Y, ntiles_of(m), P + t0 * LH * FPHE_WAVE);
+    if (hipGetLastError() != hipSuccess) return FPHE_ERR_HIP;
+  }
+  return FPHE_OK;
 }
 
 // key-holder encryption: r^n mod p^2 and mod q^2 (half-size modexps), then the CRT
@@ -639,28 +671,36 @@ fphe_status launch_encrypt_crt27(fphe_ctx* c, const uint32_t* P, uint32_t lp, co
   auto k1 = KS<TPIh>::template pow_half<L, kWinSlide, true>();
   const size_t lds1 = (size_t)kWavesPerBlock * NLh * Eh * 4;
   set_lds(k1, lds1);
-  const unsigned g1 = occ_grid(c, k1, lds1, (count + Eh - 1) / Eh, "pow_half27<enc>");
+  const size_t span = span_elems(c, k1, lds1, Eh);
+  const size_t m0 = count < span ? count : span;
+  const unsigned g1 = occ_grid(c, k1, lds1, (m0 + Eh - 1) / Eh, "pow_half27<enc>");
   const size_t tbytes = (size_t)g1 * kWavesPerBlock * kTabEntries<kWinSlide> * rad_ll(TPIh) * FPHE_WAVE * 4;
-  const size_t ybytes = (size_t)ntiles_of(count) * 2 * L1 * FPHE_WAVE * 4;
-  const size_t rbytes = (size_t)ntiles_of(count) * L1 * FPHE_WAVE * 4;
+  const size_t ybytes = (size_t)ntiles_of(m0) * 2 * L1 * FPHE_WAVE * 4;
+  const size_t rbytes = (size_t)ntiles_of(m0) * L1 * FPHE_WAVE * 4;
   if (ensure_scratch(c, tbytes + ybytes + (r ? 0 : rbytes), s) != FPHE_OK) return FPHE_ERR_HIP;
   u32* Y = c->scratch + tbytes / 4;
-  const u32* rbuf = r;
-  if (!r) {
-    u32* rdev = Y + ybytes / 4;
-    ChaChaKey ck;
+  ChaChaKey ck;
+  if (!r)
     for (int i = 0; i < 8; ++i) ck.k[i] = key[i];
-    const unsigned rgrid = (unsigned)std::min<size_t>((count + 255) / 256, (size_t)c->cus * 4);
-    hipLaunchKernelGGL(k_draw_r<L1>, dim3(rgrid), dim3(256), 0, s, c->K, count, ck, nonce, rdev);
-    rbuf = rdev;
-  }
-  hipLaunchKernelGGL(k1, dim3(g1), dim3(kBlock), lds1, s, c->K, rbuf, count, Y, c->scratch, (u32)NLh);
   auto k2 = KS<TPI>::template encrypt_crt<L>();
   const size_t lds2 = (size_t)kWavesPerBlock * LDSW * E * 4;
   set_lds(k2, lds2);
-  const unsigned g2 = occ_grid(c, k2, lds2, (count + E - 1) / E, "encrypt_crt27");
-  hipLaunchKernelGGL(k2, dim3(g2), dim3(kBlock), lds2, s, c->K, P, lp, neg, count, Y, C, sign, (u32)LDSW);
-  return hip_ok(hipGetLastError());
+  const unsigned g2 = occ_grid(c, k2, lds2, (m0 + E - 1) / E, "encrypt_crt27");
+  for (size_t e0 = 0; e0 < count; e0 += span) {
+    const size_t m = count - e0 < span ? count - e0 : span, t0 = e0 / FPHE_WAVE;
+    const u32* rbuf = r ? r + t0 * L1 * FPHE_WAVE : nullptr;
+    if (!r) {
+      u32* rdev = Y + ybytes / 4;
+      const unsigned rgrid = (unsigned)std::min<size_t>((m + 255) / 256, (size_t)c->cus * 4);
+      hipLaunchKernelGGL(k_draw_r<L1>, dim3(rgrid), dim3(256), 0, s, c->K, m, ck, nonce, e0, rdev);
+      rbuf = rdev;
+    }
+    hipLaunchKernelGGL(k1, dim3(g1), dim3(kBlock), lds1, s, c->K, rbuf, m, Y, c->scratch, (u32)NLh);
+    hipLaunchKernelGGL(k2, dim3(g2), dim3(kBlock), lds2, s, c->K, P + t0 * lp * FPHE_WAVE, lp, neg + e0, m, Y,
+                       C + t0 * L * FPHE_WAVE, sign + e0, (u32)LDSW);
+    if (hipGetLastError() != hipSuccess) return FPHE_ERR_HIP;
+  }
+  return FPHE_OK;
 }
 
 template <int L>
@@ -804,31 +844,40 @@ fphe_status launch_mul27(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, con
   auto kern = KS<TPI>::template mul<L, kWinMul>();
   const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
   set_lds(kern, lds);
-  const unsigned grid = occ_grid(c, kern, lds, (count + E - 1) / E, "mul27");
+  // spans as for encrypt: plaintexts that are encoded negative ints take k-bit exponents
+  const size_t span = span_elems(c, kern, lds, E);
+  const size_t m0 = count < span ? count : span;
+  const unsigned grid = occ_grid(c, kern, lds, (m0 + E - 1) / E, "mul27");
   // scratch: [window tables][need T*64 B][ebits T*64 i32][E T*L1*64 w][Cinv T*L*64 w][X0 T*L1*64 w]
-  const size_t nt = ntiles_of(count);
+  const size_t nt = ntiles_of(m0);
   const size_t tbytes = (size_t)grid * kWavesPerBlock * (1u << kWinMul) * rad_ll(TPI) * FPHE_WAVE * 4;
   const size_t o_need = tbytes, o_eb = o_need + nt * FPHE_WAVE, o_E = o_eb + nt * FPHE_WAVE * 4;
-  const bool batch = count >= binv_min();
   const size_t o_inv = o_E + nt * L1 * FPHE_WAVE * 4, o_x0 = o_inv + nt * L * FPHE_WAVE * 4;
-  const size_t total = o_x0 + (batch ? binv_scratch_bytes<L>(count) : nt * L1 * FPHE_WAVE * 4);
-  if (ensure_scratch(c, total, s) != FPHE_OK) return FPHE_ERR_HIP;
+  const size_t x0b = nt * L1 * FPHE_WAVE * 4, binvb = m0 >= binv_min() ? binv_scratch_bytes<L>(m0) : 0;
+  if (ensure_scratch(c, o_x0 + (binvb > x0b ? binvb : x0b), s) != FPHE_OK) return FPHE_ERR_HIP;
   char* base = reinterpret_cast<char*>(c->scratch);
   u8* need = reinterpret_cast<u8*>(base + o_need);
   int32_t* eb = reinterpret_cast<int32_t*>(base + o_eb);
   u32* Ex = reinterpret_cast<u32*>(base + o_E);
   u32* Cinv = reinterpret_cast<u32*>(base + o_inv);
   u32* X0 = reinterpret_cast<u32*>(base + o_x0);
-  const unsigned pgrid = (unsigned)std::min<size_t>((count + 255) / 256, (size_t)c->cus * 8);
-  hipLaunchKernelGGL(k_mul_prep<L>, dim3(pgrid), dim3(256), 0, s, c->K, P, lp, pneg, pstride, count, need, Ex, eb,
-                     err);
-  if (batch)
-    launch_binv27<L>(c, Ca, count, need, Cinv, err, X0, s);
-  else
-    launch_inv27<L>(c, Ca, count, need, Cinv, err, X0, s);
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, Ca, Cinv, need, ea, Ex, eb, pexp, pstride, count,
-                     Co, so, eo, c->scratch, (u32)NL);
-  return hip_ok(hipGetLastError());
+  for (size_t e0 = 0; e0 < count; e0 += span) {
+    const size_t m = count - e0 < span ? count - e0 : span, t0 = e0 / FPHE_WAVE;
+    const uint32_t* Cs = Ca + t0 * L * FPHE_WAVE;
+    const uint32_t* Ps = pstride ? P + t0 * lp * FPHE_WAVE : P;
+    const uint8_t* ns = pstride ? pneg + e0 : pneg;
+    const int32_t* xs = pstride ? pexp + e0 : pexp;
+    const unsigned pgrid = (unsigned)std::min<size_t>((m + 255) / 256, (size_t)c->cus * 8);
+    hipLaunchKernelGGL(k_mul_prep<L>, dim3(pgrid), dim3(256), 0, s, c->K, Ps, lp, ns, pstride, m, need, Ex, eb, err);
+    if (m >= binv_min())
+      launch_binv27<L>(c, Cs, m, need, Cinv, err, X0, s);
+    else
+      launch_inv27<L>(c, Cs, m, need, Cinv, err, X0, s);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, Cs, Cinv, need, ea + e0, Ex, eb, xs, pstride, m,
+                       Co + t0 * L * FPHE_WAVE, so + e0, eo + e0, c->scratch, (u32)NL);
+    if (hipGetLastError() != hipSuccess) return FPHE_ERR_HIP;
+  }
+  return FPHE_OK;
 }
 
 

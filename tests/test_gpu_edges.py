@@ -387,3 +387,61 @@ def test_add_across_launch_chunks():
         want = O.ct_add(opk, ca, cb)
         got = mo[k] - ns if so[k] and mo[k] else mo[k]
         assert (got, eo[k]) == (want.c, want.exp), idx[k]
+
+
+@pytest.mark.parametrize("keyholder", [False, True], ids=["public", "keyholder_crt"])
+def test_spans_match_one_launch(monkeypatch, keyholder):
+    """Long encrypt / decrypt calls run as spans of whole grid rounds (fate_phe.hip
+    span_elems): forced down to one round per span, a call over several spans gives the same
+    ciphertexts as one launch -- device-drawn nonces included (each element draws the stream
+    of its index in the call) -- and decrypts to the same plaintexts."""
+    p, q, sk, pk, coder, osk, opk = load(1024)
+    if not keyholder:
+        pk = P.PK(pk.n)
+    assert pk.keyholder == keyholder
+    key = pk._priv if keyholder else pk._key
+    n = 250_000 + 37  # > 2 one-round spans at 1024 bits (98,304 or 196,608 elements)
+    g = torch.Generator().manual_seed(3)
+    x = (torch.randn(n, generator=g) * 4).cuda()
+    x[-1000:] = x[:1000]  # the same plaintexts in the first and the last span
+    pv = coder.encode_f32_vec(x)
+    monkeypatch.setattr(key, "next_nonce", lambda: 4242)
+    one = pk.encrypt_encoded(pv, True)
+    d_one = sk.decrypt_to_encoded(one)
+    monkeypatch.setenv("FPHE_SPAN_TARGET", "1")
+    spans = pk.encrypt_encoded(pv, True)
+    d_spans = sk.decrypt_to_encoded(spans)
+    monkeypatch.delenv("FPHE_SPAN_TARGET")
+    # elements past the count (the last tile's padding lanes) hold unspecified words
+    assert torch.equal(P.tiles_to_cols(one.C)[:, :n], P.tiles_to_cols(spans.C)[:, :n])
+    assert torch.equal(one.sign[:n], spans.sign[:n])
+    assert torch.equal(P.tiles_to_cols(d_one.P)[:, :n], P.tiles_to_cols(d_spans.P)[:, :n])
+    y = coder.decode_f32_vec(d_spans).cpu().numpy().view(np.uint32)
+    xb = x.cpu().numpy().view(np.uint32)
+    assert (y == np.where(xb == 0x80000000, 0, xb)).all()
+    # no nonce stream repeats across spans: equal plaintexts, different ciphertexts
+    assert not torch.equal(spans.C[:15], spans.C[(n - 1000) // 64:(n - 1000) // 64 + 15])
+    cs = P.tiles_to_cols(spans.C.cpu())
+    assert not any(torch.equal(cs[:, i], cs[:, n - 1000 + i]) for i in range(64))
+
+
+def test_mul_spans_match_one_launch(monkeypatch):
+    """ct x pt split into spans (forced to one grid round each) equals one launch: per-element
+    plaintexts with negative weights (the batch inverse per span) and a broadcast scalar."""
+    p, q, sk, pk, coder, osk, opk = load(1024)
+    n = 300_000 + 11
+    g = torch.Generator().manual_seed(4)
+    x = (torch.randn(n, generator=g) * 4).cuda()
+    w = (torch.rand(n, generator=g) * 3 - 1).cuda()  # a third negative
+    ct = pk.encrypt_encoded(coder.encode_f32_vec(x), True)
+    pw = coder.encode_f32_vec(w)
+    sc = P.Plaintext(coder.encode_f32_vec(torch.tensor([-1.25], device="cuda")))
+    one, one_s = ct.mul(pk, pw), ct.mul_scalar(pk, sc)
+    monkeypatch.setenv("FPHE_SPAN_TARGET", "1")
+    sp, sp_s = ct.mul(pk, pw), ct.mul_scalar(pk, sc)
+    monkeypatch.delenv("FPHE_SPAN_TARGET")
+    for a, b in ((one, sp), (one_s, sp_s)):
+        assert torch.equal(P.tiles_to_cols(a.C)[:, :n], P.tiles_to_cols(b.C)[:, :n])
+        assert torch.equal(a.sign[:n], b.sign[:n]) and torch.equal(a.exp[:n], b.exp[:n])
+    d = coder.decode_f64_vec(sk.decrypt_to_encoded(sp)).cpu()
+    assert torch.allclose(d, (x.double() * w.double()).cpu(), rtol=1e-6, atol=1e-6)
