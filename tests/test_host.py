@@ -32,6 +32,23 @@ def test_library_exports_every_header_symbol():
     assert _lib.load() is not None
 
 
+def test_header_is_plain_c_and_links(tmp_path):
+    """include/fate_phe.h is a plain C header (what a cgo / Rust FFI binding includes) and a
+    C program linking only libfatephe.so and the HIP runtime builds against it
+    (tests/c_abi/abi_roundtrip.c, run on the GPU by tests/test_gpu_c_abi.py)."""
+    import subprocess
+    inc = os.path.join(ROOT, "include")
+    subprocess.run(["gcc", "-std=c11", "-Wall", "-Wextra", "-Werror", "-fsyntax-only", "-x", "c",
+                    os.path.join(inc, "fate_phe.h")], check=True)
+    out = tmp_path / "abi_roundtrip"
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "c_abi"), f"abi_roundtrip"], check=True)
+    subprocess.run(["gcc", "-O2", "-std=c11", "-Wall", "-Wextra", "-Werror", "-D__HIP_PLATFORM_AMD__", f"-I{inc}",
+                    "-I/opt/rocm/include", "-o", str(out), os.path.join(ROOT, "tests", "c_abi", "abi_roundtrip.c"),
+                    "-L" + os.path.join(ROOT, "fate_amd", "lib"), "-lfatephe", "-L/opt/rocm/lib", "-lamdhip64"],
+                   check=True)
+    assert out.exists()
+
+
 def test_tile_layout_roundtrip():
     from fate_amd import paillier as P
     rng = np.random.default_rng(0)
