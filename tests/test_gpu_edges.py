@@ -406,12 +406,17 @@ def test_spans_match_one_launch(monkeypatch, keyholder):
     x[-1000:] = x[:1000]  # the same plaintexts in the first and the last span
     pv = coder.encode_f32_vec(x)
     monkeypatch.setattr(key, "next_nonce", lambda: 4242)
+    rng = random.Random(17)
+    rs = [1 + rng.randrange(pk.n - 1) for _ in range(n)]  # injected nonces (parity mode)
     one = pk.encrypt_encoded(pv, True)
     d_one = sk.decrypt_to_encoded(one)
+    one_r = pk.encrypt_encoded(pv, True, r=rs)
     monkeypatch.setenv("FPHE_SPAN_TARGET", "1")
     spans = pk.encrypt_encoded(pv, True)
     d_spans = sk.decrypt_to_encoded(spans)
+    spans_r = pk.encrypt_encoded(pv, True, r=rs)
     monkeypatch.delenv("FPHE_SPAN_TARGET")
+    assert torch.equal(P.tiles_to_cols(one_r.C)[:, :n], P.tiles_to_cols(spans_r.C)[:, :n])
     # elements past the count (the last tile's padding lanes) hold unspecified words
     assert torch.equal(P.tiles_to_cols(one.C)[:, :n], P.tiles_to_cols(spans.C)[:, :n])
     assert torch.equal(one.sign[:n], spans.sign[:n])
