@@ -705,7 +705,8 @@ def main() -> None:
         "config": ({"workload": f"paillier2048_encrypt_f32_{args.total}_strong", "key_bits": key_bits,
                     "elements_total": args.total, "elements_rank0": N, "obfuscate": True,
                     "parallelism": f"shard{world}"} if strong else
-                   {"workload": "paillier2048_encrypt_f32_1M", "key_bits": key_bits, "elements_per_gpu": N,
+                   {"workload": "paillier2048_encrypt_f32_" + ("1M" if N == 1 << 20 else str(N)), "key_bits": key_bits,
+                    "elements_per_gpu": N,
                     "obfuscate": True, "parallelism": f"shard{world}"}),
         "roofline": roofline,
     }
