@@ -87,8 +87,10 @@ def gen(LL, LB):
         redm = [f"v_mad_u64_u32 {treg(j - 1)}, vcc, v11, %[n{j}], {treg(j)}" for j in range(1, LL)]
         seq.append("v_mad_u64_u32 v[6:7], vcc, v11, %[n0], v[2:3]")
         seq += redm[:x_gap]
-        seq.append(f"v_alignbit_b32 v8, v7, v6, {LB}")
-        seq.append(f"v_lshrrev_b32 v9, {LB}, v7")
+        # X >> LB as one 64-bit shift: on gfx950 v_alignbit_b32 is half rate like the
+        # 64-bit shift, so the alignbit + lshrrev pair cost 1.5 half-rate slots against 1
+        # (tools/probe/instr_probe.hip, profiles/r02/r02z12_probe_instr_rates.txt)
+        seq.append(f"v_lshrrev_b64 v[8:9], {LB}, v[6:7]")
         seq += redm[x_gap:x_gap + c_gap]
         seq.append("v_lshl_add_u64 v[2:3], v[8:9], 0, v[2:3]")
         seq += redm[x_gap + c_gap:]
