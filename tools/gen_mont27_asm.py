@@ -71,7 +71,7 @@ def gen(LL, LB):
     def treg(k):
         return "v[2:3]" if k == 0 else ("v[4:5]" if k == LL - 1 else f"%[t{k}]")
 
-    def fused(pos, spread):
+    def fused(pos, spread, carry64=True):
         m_gap, x_gap, c_gap = spread
         opm = [f"v_mad_u64_u32 {treg(k)}, vcc, %[a{k}], %[{mul}], {treg(k)}" for k, mul in pos]
         seq = []
@@ -87,10 +87,15 @@ def gen(LL, LB):
         redm = [f"v_mad_u64_u32 {treg(j - 1)}, vcc, v11, %[n{j}], {treg(j)}" for j in range(1, LL)]
         seq.append("v_mad_u64_u32 v[6:7], vcc, v11, %[n0], v[2:3]")
         seq += redm[:x_gap]
-        # X >> LB as one 64-bit shift: on gfx950 v_alignbit_b32 is half rate like the
-        # 64-bit shift, so the alignbit + lshrrev pair cost 1.5 half-rate slots against 1
-        # (tools/probe/instr_probe.hip, profiles/r02/r02z12_probe_instr_rates.txt)
-        seq.append(f"v_lshrrev_b64 v[8:9], {LB}, v[6:7]")
+        # X >> LB: one 64-bit shift (v_alignbit_b32 is half rate on gfx950 like the shift,
+        # tools/probe/instr_probe.hip) -- same-box +2.9% for the TPI-4 kernels -- or the
+        # alignbit + lshrrev pair, which the TPI-2 kernels keep (the shift measured -1% there,
+        # profiles/r02/r02z15_ab_carry_per_tpi.txt)
+        if carry64:
+            seq.append(f"v_lshrrev_b64 v[8:9], {LB}, v[6:7]")
+        else:
+            seq.append(f"v_alignbit_b32 v8, v7, v6, {LB}")
+            seq.append(f"v_lshrrev_b32 v9, {LB}, v7")
         seq += redm[x_gap:x_gap + c_gap]
         seq.append("v_lshl_add_u64 v[2:3], v[8:9], 0, v[2:3]")
         seq += redm[x_gap + c_gap:]
@@ -111,9 +116,11 @@ def gen(LL, LB):
     SPREADS = {0: (3, 2, 1), 1: (6, 8, 8)}
     spread_macros = {}
     for sp, spread in SPREADS.items():
-        lst = [("RGF_ROW(BC)", fused([(k, "b") for k in range(LL)], spread))]
-        for a in range(LL):
-            lst.append((f"RGF_SQROW_{a}(BC)", fused(window(a), spread)))
+        lst = []
+        for fam, c64 in (("RGF", True), ("RGF2", False)):  # RGF: TPI 4 rows, RGF2: TPI 2 rows
+            lst.append((f"{fam}_ROW(BC)", fused([(k, "b") for k in range(LL)], spread, c64)))
+            for a in range(LL):
+                lst.append((f"{fam}_SQROW_{a}(BC)", fused(window(a), spread, c64)))
         spread_macros[sp] = lst
 
     out = [f"// Generated by tools/gen_mont27_asm.py -- do not edit.  {LL} limbs of {LB} bits per lane.",
@@ -139,17 +146,17 @@ def gen(LL, LB):
         out.append("}")
     out.append("#elif RG_SECTION == 3")
     out.append("template <int TPI, int a> __device__ __forceinline__ void r27f_sqrow(u64 (&T)[LL], const L27& A, u32 bf, u32 bm, u32 bl, const Mod<TPI>& N, u32 np, u32 mk);")
-    tpis = ((4, "quad_perm:[0,0,0,0]"), (2, "quad_perm:[0,0,2,2]"))
+    tpis = ((4, "quad_perm:[0,0,0,0]", "RGF"), (2, "quad_perm:[0,0,2,2]", "RGF2"))
     for a in range(LL):
-        for tpi, bc in tpis:
+        for tpi, bc, fam in tpis:
             out.append(f"template <> __device__ __forceinline__ void r27f_sqrow<{tpi}, {a}>(u64 (&T)[LL], const L27& A, u32 bf, u32 bm, u32 bl, const Mod<{tpi}>& N, u32 np, u32 mk) {{")
             bl_in = ' [bl] "v"(bl),' if LL % 2 == 0 else ''
-            out.append(f'  asm volatile(RGF_SQROW_{a}("{bc}") : RGF_T_OPS(T) : RG_A_INS(A), RG_N_INS(N, "v"), [bf] "v"(bf), [bm] "v"(bm),{bl_in} [np] "s"(np), [mk] "v"(mk) : RGF_CLOB);')
+            out.append(f'  asm volatile({fam}_SQROW_{a}("{bc}") : RGF_T_OPS(T) : RG_A_INS(A), RG_N_INS(N, "v"), [bf] "v"(bf), [bm] "v"(bm),{bl_in} [np] "s"(np), [mk] "v"(mk) : RGF_CLOB);')
             out.append("}")
     out.append("template <int TPI> __device__ __forceinline__ void r27f_row(u64 (&T)[LL], const L27& A, u32 b, const Mod<TPI>& N, u32 np, u32 mk);")
-    for tpi, bc in tpis:
+    for tpi, bc, fam in tpis:
         out.append(f"template <> __device__ __forceinline__ void r27f_row<{tpi}>(u64 (&T)[LL], const L27& A, u32 b, const Mod<{tpi}>& N, u32 np, u32 mk) {{")
-        out.append(f'  asm volatile(RGF_ROW("{bc}") : RGF_T_OPS(T) : RG_A_INS(A), RG_N_INS(N, "v"), [b] "v"(b), [np] "s"(np), [mk] "v"(mk) : RGF_CLOB);')
+        out.append(f'  asm volatile({fam}_ROW("{bc}") : RGF_T_OPS(T) : RG_A_INS(A), RG_N_INS(N, "v"), [b] "v"(b), [np] "s"(np), [mk] "v"(mk) : RGF_CLOB);')
         out.append("}")
     out.append("#elif RG_SECTION == 4")
     names = {n.split("(")[0] for n, _ in macros} | {n.split("(")[0] for lst in spread_macros.values() for n, _ in lst}
