@@ -112,13 +112,19 @@ def dec_mac32_per_elem(key_bits: int) -> float:
     return 2 * (E + math.ceil(E / 5) + 16) * mac32_per_mont(L)
 
 
+def _profile_order(path: str):
+    """Natural order of profile names (r02z7 < r02z16): digit runs compare as numbers."""
+    import re
+    return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(path))]
+
+
 def pmc_traffic_per_elem():
     """HBM bytes per element of k_encrypt27 from the committed rocprofv3 PMC passes
     (FETCH_SIZE and WRITE_SIZE in separate runs, FETCH_SIZE doubled per the calibration
     probe tools/probe/fetch_calib.hip), or None when no such profile is present."""
     import glob
     paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "*pmc_encrypt27.json"), recursive=True),
-                   key=os.path.basename)
+                   key=_profile_order)
     if not paths:
         return None, None
     with open(paths[-1]) as f:
@@ -131,7 +137,7 @@ def pmc_ops_traffic(op: str):
     committed PMC passes (tools/pmc_ops_summary.py), or (None, None)."""
     import glob
     paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "*pmc_ops.json"), recursive=True),
-                   key=os.path.basename)
+                   key=_profile_order)
     if not paths:
         return None, None
     with open(paths[-1]) as f:
