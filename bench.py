@@ -35,6 +35,9 @@ KEY_FIXTURE = os.path.join(ROOT, "tests", "golden", "paillier_2048.json")
 # (measured half rate in profiles/r01_probe_alu.txt); one MAC32 = 32x32->64 multiply-add.
 PEAK_TMAC32 = 256 * 128 * 2.4e9 / 2 / 1e12
 PEAK_HBM_GBS = 8000.0
+# host CPUs one GPU's box may use (the pool's share per GPU of an 8-GPU host); the CPU
+# baseline's worker pool is capped there and the whole host is projected from it
+CPU_SHARE_PER_GPU = 16
 # limbs per lane of the Montgomery engine (28-bit limbs, fate_amd/csrc/mont27_dev.h)
 ENGINE_LL = 37
 
@@ -158,7 +161,8 @@ def cpu_baseline(p: int, q: int, seconds: float = 3.0):
     workers must not inherit this GPU-initialised process."""
     import subprocess
     procs = int(os.environ.get("FPHE_CPU_PROCS", "0"))
-    cmd = [sys.executable, "-m", "oracle.cpu_baseline", "--p", hex(p), "--q", hex(q), "--seconds", str(seconds)]
+    cmd = [sys.executable, "-m", "oracle.cpu_baseline", "--p", hex(p), "--q", hex(q), "--seconds", str(seconds),
+           "--max-procs", str(CPU_SHARE_PER_GPU)]
     if procs:
         cmd += ["--procs", str(procs)]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600)
@@ -171,13 +175,22 @@ def cpu_baseline(p: int, q: int, seconds: float = 3.0):
         "unit": "encrypts/s",
         "cores": d["procs"],
         "kind": "port",
-        "per_core": ops["encrypt"]["per_core_per_s"],
+        "per_core": ops["encrypt"]["per_process_per_s"],
+        "single_process_per_s": {k: ops[k]["single_process_per_s"] for k in ops},
         "decrypt_per_s": ops["decrypt"]["per_s"],
         "ct_add_per_s": ops["add"]["per_s"],
         "ct_add_hetero_lr_gaps_per_s": ops["add_gap"]["per_s"],
         "cpu_model": d["cpu_model"],
         "machine_cores": d["machine_cores"],
         "usable_cores": d["usable_cores"],
+        "cgroup_cpu_max": d["cgroup_cpu_max"],
+        "cpu_share": {"cores": d["procs"], "affinity": d["usable_cores"], "cgroup_quota_cpus": d["cgroup_quota_cpus"],
+                      "rule": (f"the GPU box is a 1-GPU slice of an {d['topology']['hw_threads']}-thread host whose "
+                               f"CPU share per GPU is {CPU_SHARE_PER_GPU} (pool rule; no cgroup quota enforces it "
+                               f"when cgroup_quota_cpus is null), so worker pools stay at that share")},
+        "topology": d["topology"],
+        "smt": d["smt"],
+        "host_projection": d["host_projection"],
         "sample": (f"{d['procs']} worker processes (one per core, FATE's process pool), libgmp mpz_* in the "
                    f"reference's call order (oracle/gmp_ref.c), 2048-bit key: {ops['encrypt']['elements']} "
                    f"obfuscated encryptions, {ops['decrypt']['elements']} CRT decryptions, "
@@ -558,20 +571,9 @@ def main() -> None:
             # partial histograms are all-gathered over RCCL and folded again with ct-add
             # (RCCL has no modular product; ciphertext folds are order independent)
             try:
-                from fate_amd.dist import gather_tiles
+                from fate_amd.dist import fold_across_ranks
                 barrier()
-                tg = time.perf_counter()
-                Cg, sg, eg, total = gather_tiles(hist.C, hist.sign, hist.exp, hist.count)
-                barrier()
-                t_gather = time.perf_counter() - tg
-                allp = P.CiphertextVector(Cg, sg, eg, total)
-                m = hist.count
-                tf = time.perf_counter()
-                acc = allp.slice(0, m)
-                for r in range(1, world):
-                    acc = acc.add(pk, allp.slice(r * m, m))
-                torch.cuda.synchronize(dev)
-                t_fold = time.perf_counter() - tf
+                acc, t_gather, t_fold = fold_across_ranks(pk, hist)
                 wants = [torch.zeros_like(want) for _ in range(world)]
                 tdist.all_gather_object(wants, want)
                 want_all = sum(wants)
@@ -580,7 +582,7 @@ def main() -> None:
                 hist_mgpu = {"ranks": world, "gather_s": round(t_gather, 4), "fold_s": round(t_fold, 4),
                              "allclose": bool(torch.allclose(got_all[fin_all], want_all[fin_all], rtol=1e-9,
                                                              atol=1e-6))}
-                del Cg, sg, eg, allp, acc
+                del acc
             except Exception as exc:  # report, do not take the scaling run down
                 hist_mgpu = {"error": repr(exc)[:200]}
         packed = hist_packed_leg(P, pk_kh, sk, coder, N, HF, NB, key_bits, rank, dev)
@@ -720,7 +722,22 @@ def main() -> None:
     out.update(extras)
     if world == 1 and not args.no_cpu_baseline and not strong:
         try:
-            out["cpu_baseline"] = cpu_baseline(p, q)
+            cb = cpu_baseline(p, q)
+            # GPU / CPU ratios: against the measured worker pool, one process, and the
+            # projected whole host (north_star target: >= 10x on 2048-bit encrypt)
+            sp = cb["single_process_per_s"]
+            hp = cb["host_projection"]["encrypt_per_s"]
+            ratios = {"encrypt_vs_pool": value / cb["value"], "encrypt_vs_1_process": value / sp["encrypt"],
+                      "encrypt_vs_host_projection": value / hp if hp else None}
+            if extras:
+                ratios.update({"decrypt_vs_pool": extras["decrypt_per_s"] / cb["decrypt_per_s"],
+                               "ct_add_hetero_lr_vs_pool": extras["ct_add_per_s"] / cb["ct_add_hetero_lr_gaps_per_s"],
+                               "decrypt_vs_host_projection": extras["decrypt_per_s"] / (cb["decrypt_per_s"] * hp
+                                                                                         / cb["value"]),
+                               "ct_add_hetero_lr_vs_host_projection": extras["ct_add_per_s"] / (
+                                   cb["ct_add_hetero_lr_gaps_per_s"] * hp / cb["value"])})
+            cb["gpu_over_cpu"] = {k: (round(v, 2) if v is not None else None) for k, v in ratios.items()}
+            out["cpu_baseline"] = cb
         except Exception as exc:  # GMP missing on the box: say so, do not fake a number
             out["cpu_baseline"] = {"value": None, "unit": "encrypts/s", "cores": 0, "kind": "port",
                                    "sample": f"unavailable: {exc}"}

@@ -90,6 +90,10 @@ __device__ __forceinline__ ColIO colio(const u32* tile_base, u32 rows, u32 col, 
 }
 
 constexpr int kFoldMax = 64;  // terms per k_fold27 chunk (host: R^k fix-up factors)
+// largest exponent gap k_add27 / k_align27 act on (4 kMaxGap squarings, ~7 s on one wave):
+// far beyond the reference encoders' exponent range (f64: [-282, 242]); fphe_align rejects
+// larger gaps on the host side (fate_amd/paillier.py), k_add27 caps them
+constexpr int kMaxGap = 1 << 16;
 
 // ======================================================================================
 // ct x pt (fixedpoint_paillier/src/lib.rs:334-349), 27-bit engine, per-element exponents.

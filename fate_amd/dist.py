@@ -7,13 +7,14 @@ Paillier encrypt / decrypt / ct-add / ct x pt are independent per element, so a 
 partitions.  The only exchange step is the optional all-gather of the ciphertext shards
 when the consumer needs the whole vector in one place (e.g. the federation sender on rank
 0): one ``all_gather_into_tensor`` of the byte-packed tiles per component, over RCCL/xGMI
-on GPUs (backend "nccl") or gloo on CPU.  Reductions across ranks would be gather-then-
-modmul (RCCL has no modular-product reduce); ciphertext reductions are order independent
+on GPUs (backend "nccl") or gloo on CPU.  Reductions across ranks are gather-then-modmul
+(RCCL has no modular-product reduce), as the reference's ``map_reduce_shard(..., add)``
+(_tensor.py:387-395) reduces per-partition partials; ciphertext folds are order independent
 (SURVEY.md §0 fact 3), so that stays bit-exact.
 """
 from __future__ import annotations
 
-from typing import Tuple
+from typing import List, Tuple
 
 import torch
 
@@ -31,14 +32,65 @@ def shard_bounds(count: int, rank: int, world: int) -> Tuple[int, int]:
     return min(t0 * WAVE, count), min(t1 * WAVE, count)
 
 
+def _pad_tiles(t: torch.Tensor, nt: int) -> torch.Tensor:
+    if t.shape[0] == nt:
+        return t.contiguous()
+    out = t.new_zeros((nt,) + tuple(t.shape[1:]))
+    out[: t.shape[0]] = t[:nt]
+    return out
+
+
+def _pad_flat(t: torch.Tensor, n: int) -> torch.Tensor:
+    if t.shape[0] == n:
+        return t.contiguous()
+    out = t.new_zeros(n)
+    m = min(n, t.shape[0])
+    out[:m] = t[:m]
+    return out
+
+
+def compact_gathered(Cg: torch.Tensor, sg: torch.Tensor, eg: torch.Tensor, counts: List[int]):
+    """The gathered, per-rank padded shards (rank r's shard at tiles [r * nt_max, ...)) as
+    one vector, elements in rank order.  Returns (C, sign, exp, total).  Whole-tile shards
+    (shard_bounds) are concatenated tile by tile; ragged shards (e.g. per-rank partial
+    histograms of any slot count) by an element gather of the valid slots."""
+    world = len(counts)
+    nt_max = Cg.shape[0] // max(world, 1)
+    L = Cg.shape[1]
+    dev = Cg.device
+    total = sum(counts)
+    if all(c == nt_max * WAVE for c in counts[:-1]) and (counts[-1] + WAVE - 1) // WAVE == nt_max:
+        return Cg, sg, eg, total  # no padding tiles (only the last shard's own partial tile)
+    if all(c % WAVE == 0 for c in counts[:-1]):
+        Cs, ss, es = [], [], []
+        for r, c in enumerate(counts):
+            nt = (c + WAVE - 1) // WAVE
+            Cs.append(Cg[r * nt_max: r * nt_max + nt])
+            ss.append(sg[r * nt_max * WAVE: r * nt_max * WAVE + nt * WAVE])
+            es.append(eg[r * nt_max * WAVE: r * nt_max * WAVE + nt * WAVE])
+        return torch.cat(Cs), torch.cat(ss), torch.cat(es), total
+    # ragged: rank r's element k sits at r * nt_max * 64 + k of the gathered tiles
+    idx = torch.cat([torch.arange(c, device=dev) + r * nt_max * WAVE for r, c in enumerate(counts)])
+    rows = Cg.permute(0, 2, 1).reshape(-1, L)[idx]
+    nt = (total + WAVE - 1) // WAVE
+    Cf = rows.new_zeros((nt * WAVE, L))
+    Cf[:total] = rows
+    sf = sg.new_zeros(nt * WAVE)
+    sf[:total] = sg[idx]
+    ef = eg.new_zeros(nt * WAVE)
+    ef[:total] = eg[idx]
+    return Cf.view(nt, WAVE, L).permute(0, 2, 1).contiguous(), sf, ef, total
+
+
 def gather_tiles(C: torch.Tensor, sign: torch.Tensor, exp: torch.Tensor, count: int, group=None,
                  trim: bool = True):
-    """All-gather the per-rank shards (tile-major C [nt, L, 64], sign/exp [nt*64]) into the
-    full vector on every rank, elements in rank order.  Shards are padded to the largest
-    shard for the collective and, with ``trim``, the padding is cut out after (one copy of
-    the gathered vector; ragged shards by an element gather).  Returns (C, sign, exp, total_count); with ``trim=False`` the padded buffers
-    as gathered ([world * nt_max] tiles, rank r's shard at tiles [r * nt_max, ...)) and the
-    per-rank counts instead of the total."""
+    """All-gather the per-rank shards (tile-major C [nt, L, 64], sign uint8 / exp int32
+    [nt*64]) into the full vector on every rank, elements in rank order: three
+    ``all_gather_into_tensor`` calls (limbs, one byte of sign, exponent per element) over
+    RCCL on GPU tensors.  Shards are padded to the largest shard for the collective and, with
+    ``trim``, the padding is cut out after (:func:`compact_gathered`).  Returns (C, sign, exp,
+    total_count); with ``trim=False`` the padded buffers as gathered ([world * nt_max] tiles)
+    and the per-rank counts instead of the total."""
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
@@ -49,62 +101,66 @@ def gather_tiles(C: torch.Tensor, sign: torch.Tensor, exp: torch.Tensor, count: 
     counts = [int(c.item()) for c in counts]
     nt_max = max((c + WAVE - 1) // WAVE for c in counts) if counts else 0
     L = C.shape[1]
-
-    def pad_tiles(t: torch.Tensor) -> torch.Tensor:
-        if t.shape[0] == nt_max:
-            return t.contiguous()
-        out = t.new_zeros((nt_max,) + tuple(t.shape[1:]))
-        out[: t.shape[0]] = t
-        return out
-
-    def pad_flat(t: torch.Tensor) -> torch.Tensor:
-        n = nt_max * WAVE
-        if t.shape[0] == n:
-            return t.contiguous()
-        out = t.new_zeros(n)
-        out[: t.shape[0]] = t
-        return out
-
     Cg = torch.empty((world * nt_max, L, WAVE), dtype=C.dtype, device=dev)
-    dist.all_gather_into_tensor(Cg, pad_tiles(C), group=group)
-    # sign is uint8: gather as int32 for backend portability (gloo lacks uint8 on some builds)
-    sg = torch.empty(world * nt_max * WAVE, dtype=torch.int32, device=dev)
-    dist.all_gather_into_tensor(sg, pad_flat(sign.to(torch.int32)), group=group)
+    dist.all_gather_into_tensor(Cg, _pad_tiles(C, nt_max), group=group)
+    sg = torch.empty(world * nt_max * WAVE, dtype=torch.uint8, device=dev)
+    dist.all_gather_into_tensor(sg, _pad_flat(sign.to(torch.uint8), nt_max * WAVE), group=group)
     eg = torch.empty(world * nt_max * WAVE, dtype=exp.dtype, device=dev)
-    dist.all_gather_into_tensor(eg, pad_flat(exp), group=group)
+    dist.all_gather_into_tensor(eg, _pad_flat(exp, nt_max * WAVE), group=group)
     if not trim:
         return Cg, sg, eg, counts
-    total = sum(counts)
-    if all(c == nt_max * WAVE for c in counts[:-1]) and (counts[-1] + WAVE - 1) // WAVE == nt_max:
-        # no padding tiles (only the last shard's partial tile, which is the vector's end)
-        return Cg, sg.to(torch.uint8), eg, total
-    if all(c % WAVE == 0 for c in counts[:-1]):
-        # whole-tile shards (shard_bounds): drop the per-rank padding tiles
-        Cs, ss, es = [], [], []
-        for r, c in enumerate(counts):
-            nt = (c + WAVE - 1) // WAVE
-            Cs.append(Cg[r * nt_max: r * nt_max + nt])
-            ss.append(sg[r * nt_max * WAVE: r * nt_max * WAVE + nt * WAVE])
-            es.append(eg[r * nt_max * WAVE: r * nt_max * WAVE + nt * WAVE])
-        return torch.cat(Cs), torch.cat(ss).to(torch.uint8), torch.cat(es), total
-    # ragged shards (e.g. per-rank partial histograms of any slot count): element gather of
-    # the valid slots, rank r's element k sitting at r * nt_max * 64 + k of the gathered tiles
-    idx = torch.cat([torch.arange(c, device=dev) + r * nt_max * WAVE for r, c in enumerate(counts)])
-    rows = Cg.permute(0, 2, 1).reshape(-1, L)[idx]
-    nt = (total + WAVE - 1) // WAVE
-    Cf = rows.new_zeros((nt * WAVE, L))
-    Cf[:total] = rows
-    sf = sg.new_zeros(nt * WAVE)
-    sf[:total] = sg[idx]
-    ef = eg.new_zeros(nt * WAVE)
-    ef[:total] = eg[idx]
-    return Cf.view(nt, WAVE, L).permute(0, 2, 1).contiguous(), sf.to(torch.uint8), ef, total
+    return compact_gathered(Cg, sg, eg, counts)
 
 
 def gather_ciphertexts(cv, group=None):
     """All-gather a sharded ``fate_amd.paillier.CiphertextVector`` (every shard but the last
-    must be whole tiles, as produced by :func:`shard_bounds`)."""
+    must be whole tiles, as produced by :func:`shard_bounds`).  The key stamp travels."""
     from .paillier import CiphertextVector
 
     C, s, e, n = gather_tiles(cv.C, cv.sign, cv.exp, cv.count, group)
-    return CiphertextVector(C, s, e, n)
+    return CiphertextVector(C, s, e, n, cv.n, cv.raw)
+
+
+def fold_partials(pk, parts, nparts: int, m: int):
+    """Fold ``nparts`` partial vectors of ``m`` slots each, laid end to end in ``parts`` (part
+    r's slot j at r * m + j): out[j] = add(... add(parts[j], parts[m + j]) ...), with the
+    device segmented fold (the same path as iupdate), bit-exact with the sequential ct-add
+    chain by the order independence of the fold."""
+    from .paillier import CiphertextVector, _fold_segments
+
+    dev = parts.device
+    if nparts == 1:
+        return parts.slice(0, m)
+    seg = torch.arange(nparts * m, device=dev) % m
+    folded, ids = _fold_segments(pk, parts, seg)
+    out = CiphertextVector.zeros(m, pk._key.L2, dev)
+    out._assign(ids, folded)
+    out.n = pk.n
+    return out
+
+
+def fold_across_ranks(pk, hist, group=None):
+    """BASELINE config 4 across GPUs: every rank folded its own samples
+    into ``hist`` (m slots); the partial histograms are all-gathered over RCCL and folded
+    slot by slot, in rank order, on every rank.  Returns (folded vector, gather seconds,
+    fold seconds)."""
+    import time
+
+    import torch.distributed as dist
+
+    from .paillier import CiphertextVector
+
+    dev = hist.device
+    world = dist.get_world_size(group)
+    torch.cuda.synchronize(dev) if dev.type == "cuda" else None
+    t0 = time.perf_counter()
+    Cg, sg, eg, total = gather_tiles(hist.C, hist.sign, hist.exp, hist.count, group)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if total != world * hist.count:
+        raise ValueError("fold_across_ranks: every rank must hold the same number of slots")
+    folded = fold_partials(pk, CiphertextVector(Cg, sg, eg, total, pk.n), world, hist.count)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    return folded, t1 - t0, time.perf_counter() - t1

@@ -236,6 +236,12 @@ def _key_for(n: int, p: Optional[int] = None, q: Optional[int] = None) -> _KeyCt
 # ints) and read back from any sequence of ints.  The state here is `bytes` (accepted by the
 # reference's __setstate__, which extracts Vec<u8> from any sequence; pickles 8x smaller than
 # a list); FPHE_PICKLE_STATE=list gives the reference's exact list form.
+#
+# A reference ciphertext vector's state is key-less: signed integers (paillier.rs:219-226).
+# Unpickled here it stays in that form ("raw": C holds the magnitudes, sign the negative
+# flags) until an operation supplies the key -- every arithmetic op takes the PK, and decrypt
+# the SK -- which converts it to (C mod n^2, sign) on the device.  Permutations (slice,
+# shuffle, cat, ...) move raw elements as they are.  No key is ever guessed.
 _UNPICKLED = threading.local()
 
 
@@ -249,18 +255,10 @@ def _isqrt_exact(ns: int) -> Optional[int]:
     return r if r * r == ns else None
 
 
-def _only_key_n(L2: int) -> Optional[int]:
-    """The modulus of the only key of this size in the process, else None."""
-    with _KEYS_LOCK:
-        ns = {n for (n, _), k in _KEYS.items() if k.L2 == L2}
-    return ns.pop() if len(ns) == 1 else None
-
-
 class unpickle_key:
-    """``with unpickle_key(pk): pickle.loads(...)`` -- the key a ciphertext vector's state is
-    read under (its signed integers become (C mod n^2, sign)).  Without it: the PK unpickled
-    last in this thread (a PHETensor pickles its PK before its data), else the only key of
-    the matching size in the process."""
+    """``with unpickle_key(pk): pickle.loads(...)`` -- read ciphertext vector states under this
+    key right away (their signed integers become (C mod n^2, sign) during the load).  Without
+    it a vector is converted when the first operation hands it a key."""
 
     def __init__(self, pk: "PK"):
         self.n = pk.n
@@ -275,19 +273,38 @@ class unpickle_key:
         return False
 
 
-def _unpickle_n(buf: bytes) -> int:
-    forced = getattr(_UNPICKLED, "forced", None)
-    if forced is not None:
-        return forced
-    last = getattr(_UNPICKLED, "n", None)
-    if last is not None:
-        return last
-    with _KEYS_LOCK:
-        ns = sorted({n for (n, _) in _KEYS})
-    if len(ns) == 1:
-        return ns[0]
-    raise TypeError("CiphertextVector state: no key to read it under (unpickle its PK first, or use "
-                    "fate_amd.paillier.unpickle_key(pk))")
+def _resolve(v: "CiphertextVector", n: int) -> None:
+    """Give a raw (unpickled, key-less) vector its key: the signed integers become (C mod n^2,
+    sign) in place (fphe_import_signed); |value| >= n^2 raises ValueError as a corrupt state."""
+    if not getattr(v, "raw", False):
+        return
+    from .wire import _check_below
+    key = _key_for(n)
+    L2 = key.L2
+    dev = v.device
+    rows = tiles_to_cols(v.C).t()[: v.count]  # [count, Lw] element-major magnitudes
+    if rows.shape[1] > L2:
+        if bool((rows[:, L2:] != 0).any()):
+            raise ValueError("CiphertextVector state: |value| >= n^2")
+        rows = rows[:, :L2]
+    elif rows.shape[1] < L2:
+        rows = torch.cat([rows, rows.new_zeros((rows.shape[0], L2 - rows.shape[1]))], 1)
+    rows = rows.contiguous()
+    if v.count:
+        _check_below(rows, n * n)
+    cv = CiphertextVector.import_signed(PK(n), rows, v.sign[: v.count].contiguous(), v.exp[: v.count])
+    v.C, v.sign, v.exp, v.n, v.raw = cv.C, cv.sign, cv.exp, n, False
+    del dev
+
+
+def _resolve_args(n: int, *objs) -> None:
+    for a in objs:
+        if isinstance(a, CiphertextVector):
+            _resolve(a, n)
+        elif isinstance(a, Ciphertext):
+            _resolve(a.vec, n)
+        elif isinstance(a, (list, tuple)):
+            _resolve_args(n, *a)
 
 
 def _fit_limbs(v: "CiphertextVector", L2: int) -> "CiphertextVector":
@@ -299,7 +316,7 @@ def _fit_limbs(v: "CiphertextVector", L2: int) -> "CiphertextVector":
         C = v.C[:, :L2, :].contiguous()
     else:
         C = torch.cat([v.C, v.C.new_zeros((v.C.shape[0], L2 - v.L2, WAVE))], dim=1)
-    return CiphertextVector(C, v.sign, v.exp, v.count, v.n)
+    return CiphertextVector(C, v.sign, v.exp, v.count, v.n, v.raw)
 
 
 _ERR_MESSAGES = [
@@ -411,12 +428,13 @@ class CiphertextVector:
     exp (base-16 exponent)."""
 
     # n: the key's modulus once known (set by encrypt and by every op that takes a PK);
-    # pickling needs it to write the reference's signed integers C - n^2
-    __slots__ = ("C", "sign", "exp", "count", "n")
+    # pickling needs it to write the reference's signed integers C - n^2.  raw: an unpickled
+    # vector not yet given its key (C = magnitudes, sign = negative flags; see _resolve)
+    __slots__ = ("C", "sign", "exp", "count", "n", "raw")
 
     def __init__(self, C: torch.Tensor = None, sign: torch.Tensor = None, exp: torch.Tensor = None, count: int = 0,
-                 n: Optional[int] = None):
-        self.C, self.sign, self.exp, self.count, self.n = C, sign, exp, count, n
+                 n: Optional[int] = None, raw: bool = False):
+        self.C, self.sign, self.exp, self.count, self.n, self.raw = C, sign, exp, count, n, raw
 
     # ---- construction / host views -----------------------------------------------
     @property
@@ -451,12 +469,18 @@ class CiphertextVector:
         v.C[:, 0, :] = 1
         return v
 
-    def to_signed_ints(self, ns: int) -> Tuple[List[int], List[int]]:
-        """Reference (signed rug::Integer, exp) pairs, for parity checks and the wire."""
+    def to_signed_ints(self, ns: Optional[int] = None) -> Tuple[List[int], List[int]]:
+        """Reference (signed rug::Integer, exp) pairs, for parity checks and the wire (ns may
+        be omitted for a raw vector, or one whose signs are all 0)."""
         rows = tiles_to_rows(self.C.cpu().numpy().view(np.uint32), self.count)
         mags = limbs_to_ints(rows)
         sg = self.sign[: self.count].cpu().numpy()
-        out = [m - ns if (s and m) else m for m, s in zip(mags, sg)]
+        if self.raw:
+            out = [-m if s else m for m, s in zip(mags, sg)]
+        else:
+            if ns is None and sg.any():
+                raise TypeError("to_signed_ints: negative elements need the key's n^2")
+            out = [m - ns if (s and m) else m for m, s in zip(mags, sg)]
         return out, self.exp[: self.count].cpu().tolist()
 
     @staticmethod
@@ -474,6 +498,7 @@ class CiphertextVector:
         """The reference's signed integers on the device (fphe_export_signed): magnitudes as
         element-major LSF uint32 words [count, L2], negative flags [count], exponents."""
         dev = self.device
+        _resolve(self, pk.n)
         v = _fit_limbs(self, pk._key.L2)
         mag = torch.empty((self.count, v.L2), dtype=torch.int32, device=dev)
         neg = torch.empty(self.count, dtype=torch.uint8, device=dev)
@@ -498,22 +523,37 @@ class CiphertextVector:
         return out
 
     # ---- pickling: the reference's state, bincode(CiphertextVector) (paillier.rs:219-226) --
+    def signed_rows(self) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        """The reference's signed integers as (element-major magnitudes [count, L2], negative
+        flags, exps) on the device, from the key this vector carries (a raw vector, or one
+        with no negative element, needs none)."""
+        if self.raw or (self.n is None and not bool(self.sign[: self.count].any())):
+            mag = tiles_to_cols(self.C).t()[: self.count].contiguous()
+            return mag, self.sign[: self.count].contiguous(), self.exp[: self.count].clone()
+        if self.n is None:
+            raise TypeError("CiphertextVector: negative elements and no key; build it through a PK operation "
+                            "before pickling")
+        return self.export_signed(PK(self.n))
+
     def __getstate__(self):
         from . import wire
-        n = self.n if self.n is not None else _only_key_n(self.L2)
-        if n is None:
-            raise TypeError("CiphertextVector: key unknown (several keys of this size in the process); "
-                            "build it through a PK operation before pickling")
-        return _pickle_state(wire.ciphertext_vector_to_bincode(self, PK(n)))
+        return _pickle_state(wire.ciphertext_vector_to_bincode(self))
 
     def __setstate__(self, state):
         from . import wire
         buf = bytes(state)
-        n = _unpickle_n(buf)
-        v, used = wire.ciphertext_vector_from_bincode(buf, PK(n))
+        forced = getattr(_UNPICKLED, "forced", None)
+        v, used = wire.ciphertext_vector_from_bincode(buf, PK(forced) if forced is not None else None)
         if used != len(buf):
             raise ValueError("bincode CiphertextVector: trailing bytes")
-        self.C, self.sign, self.exp, self.count, self.n = v.C, v.sign, v.exp, v.count, n
+        self.C, self.sign, self.exp, self.count, self.n, self.raw = v.C, v.sign, v.exp, v.count, v.n, v.raw
+
+    def __copy__(self) -> "CiphertextVector":
+        """A device-side clone (the key and raw state travel; no wire round trip)."""
+        return CiphertextVector(self.C.clone(), self.sign.clone(), self.exp.clone(), self.count, self.n, self.raw)
+
+    def __deepcopy__(self, memo) -> "CiphertextVector":
+        return self.__copy__()
 
     # ---- element plumbing (torch indexing; no arithmetic) ---------------------------
     def _gather(self, idx: torch.Tensor) -> "CiphertextVector":
@@ -522,7 +562,7 @@ class CiphertextVector:
         dev = self.device
         out = CiphertextVector(torch.zeros((nt, self.L2, WAVE), dtype=torch.int32, device=dev),
                                torch.zeros(nt * WAVE, dtype=torch.uint8, device=dev),
-                               torch.zeros(nt * WAVE, dtype=torch.int32, device=dev), n)
+                               torch.zeros(nt * WAVE, dtype=torch.int32, device=dev), n, self.n, self.raw)
         _permute(self.C, self.sign, self.exp, self.L2, idx, self.count, False, out.C, out.sign, out.exp, dev)
         return out
 
@@ -531,6 +571,13 @@ class CiphertextVector:
         idx = idx.to(self.device, torch.long)
         if idx.numel() == 0:
             return
+        if src.raw != self.raw:
+            if self.n is not None:
+                _resolve(src, self.n)
+            elif src.n is not None:
+                _resolve(self, src.n)
+            else:
+                raise TypeError("assigning between an unpickled (key-less) vector and a keyed one without a key")
         if self.L2 != src.L2:
             # a zeros() vector is sized before the key is known (evaluator.zeros(size, dtype),
             # protocol/phe/paillier.py:347-349): adopt the key's limb count, exactly
@@ -556,7 +603,7 @@ class CiphertextVector:
     def shuffle(self, indexes: Sequence[int]) -> "CiphertextVector":
         """``CiphertextVector::shuffle`` (lib.rs:492-497): result[i] = data[indexes[i]] for a
         permutation, realised as a gather (same result as the reference's cycle walk)."""
-        out = CiphertextVector(self.C.clone(), self.sign.clone(), self.exp.clone(), self.count)
+        out = CiphertextVector(self.C.clone(), self.sign.clone(), self.exp.clone(), self.count, self.n, self.raw)
         out.i_shuffle(indexes)
         return out
 
@@ -839,16 +886,18 @@ def _keyed(fn):
 
     @functools.wraps(fn)
     def w(self, *args, **kw):
-        r = fn(self, *args, **kw)
         pk = next((a for a in itertools.chain(args, kw.values()) if isinstance(a, PK)), None)
+        if pk is not None:  # unpickled operands get their key before any arithmetic
+            _resolve_args(pk.n, self, *args, *kw.values())
+        r = fn(self, *args, **kw)
         n = pk.n if pk is not None else self.n
-        if n is not None:
+        if n is not None and not self.raw:
             if self.n is None:
                 self.n = n
             for v in (r if isinstance(r, list) else [r]):
-                if isinstance(v, CiphertextVector) and v.n is None:
+                if isinstance(v, CiphertextVector) and v.n is None and not v.raw:
                     v.n = n
-                elif isinstance(v, Ciphertext) and v.vec.n is None:
+                elif isinstance(v, Ciphertext) and v.vec.n is None and not v.vec.raw:
                     v.vec.n = n
         return r
     return w
@@ -1029,6 +1078,7 @@ def _is_literal_one(v: CiphertextVector) -> torch.Tensor:
 # the pairwise ct-add tree (False: ceil(log2(partials)) launches, each as long as its largest
 # exponent gap)
 MERGE_BY_ALIGN = True
+MAX_GAP = 1 << 16  # kMaxGap of fate_amd/csrc/kernels27.h
 
 
 def _merge_exponents(pk: "PK", cur: CiphertextVector, ckeys: torch.Tensor) -> Tuple[CiphertextVector, torch.Tensor]:
@@ -1053,6 +1103,8 @@ def _merge_exponents(pk: "PK", cur: CiphertextVector, ckeys: torch.Tensor) -> Tu
     emin.scatter_reduce_(0, inv, torch.where(lit, torch.full_like(exp, big), exp), reduce="amin")
     em = emin[inv]
     gap = torch.where(lit | (em == big), torch.zeros_like(exp), exp - em)
+    if int(gap.max()) > MAX_GAP:  # fphe_align's contract (kMaxGap in kernels27.h)
+        raise ValueError(f"exponent gap beyond {MAX_GAP} (4 x {MAX_GAP} squarings per term): corrupt exponents")
     tgt = torch.where(em == big, torch.zeros_like(em), em)
     order = torch.argsort(gap, descending=True, stable=True)
     src = cur._gather(order)
@@ -1259,7 +1311,6 @@ class PK:
         from . import wire
         self._priv = None
         self._init(wire.pk_from_bincode(bytes(state)).n)
-        _UNPICKLED.n = self.n  # the key of the ciphertext vectors that follow it in a pickle
 
 
 class SK:
@@ -1280,6 +1331,7 @@ class SK:
         """``SK.decrypt_to_encoded`` (paillier.rs:79-81 -> lib.rs:392-399)."""
         dev = data.device
         k = self._key
+        _resolve(data, self.n)
         data = _fit_limbs(data, k.L2)
         n = data.count
         nt = _ntiles(n)
@@ -1503,8 +1555,17 @@ class Evaluator:
 
     @staticmethod
     def cat(vec_list: Sequence[CiphertextVector]) -> CiphertextVector:
+        n = next((v.n for v in vec_list if v.n is not None), None)
+        if n is not None:  # key-less unpickled parts join a keyed vector under its key
+            _resolve_args(n, list(vec_list))
+        elif any(v.raw for v in vec_list) and not all(v.raw for v in vec_list if v.count):
+            # raw parts beside key-less keyed parts (e.g. zeros()): only sign-0 parts can go raw
+            for v in vec_list:
+                if not v.raw and bool(v.sign[: v.count].any()):
+                    raise TypeError("cat of an unpickled (key-less) vector with a vector of unknown key")
         out = Evaluator._cat(vec_list)
-        out.n = next((v.n for v in vec_list if v.n is not None), None)
+        out.n = n
+        out.raw = n is None and any(v.raw for v in vec_list if v.count)
         return out
 
     @staticmethod
@@ -1512,6 +1573,8 @@ class Evaluator:
         vecs = [v for v in vec_list if v.count > 0]
         if not vecs:
             return CiphertextVector.zeros(0, vec_list[0].L2 if vec_list else 128)
+        L2 = max(v.L2 for v in vecs)
+        vecs = [_fit_limbs(v, L2) for v in vecs]
         n = sum(v.count for v in vecs)
         if all(v.count % WAVE == 0 for v in vecs[:-1]):  # tile-aligned: concatenate tiles as they are
             C = torch.cat([v.C[: _ntiles(v.count)] for v in vecs], dim=0)
@@ -1519,7 +1582,6 @@ class Evaluator:
                                     _pad_flat(torch.cat([v.sign[: v.count] for v in vecs]), n),
                                     _pad_flat(torch.cat([v.exp[: v.count] for v in vecs]), n), n)
         # otherwise each part is scattered to its offset (fphe_permute)
-        L2 = max(v.L2 for v in vecs)
         dev = vecs[0].device
         nt = _ntiles(n)
         out = CiphertextVector(torch.zeros((nt, L2, WAVE), dtype=torch.int32, device=dev),
@@ -1527,7 +1589,8 @@ class Evaluator:
                                torch.zeros(nt * WAVE, dtype=torch.int32, device=dev), n)
         off = 0
         for v in vecs:
-            out._assign(torch.arange(off, off + v.count, device=dev), _fit_limbs(v, L2))
+            _permute(v.C, v.sign, v.exp, L2, torch.arange(off, off + v.count, device=dev), n, True, out.C, out.sign,
+                     out.exp, dev)
             off += v.count
         return out
 

@@ -168,16 +168,17 @@ def plaintext_vector_from_bincode(buf: bytes, device=None) -> PlaintextVector:
 
 
 # ---- ciphertext vectors, on the device --------------------------------------------------
-def ciphertext_vector_to_bincode(cv: CiphertextVector, pk: PK) -> bytes:
+def ciphertext_vector_to_bincode(cv: CiphertextVector, pk: Optional[PK] = None) -> bytes:
     """``CiphertextVector {data: Vec<Ciphertext {significant_encryped, exp}>}``
-    (fixedpoint_paillier/src/lib.rs:237-241,353-356) of the reference's signed integers."""
+    (fixedpoint_paillier/src/lib.rs:237-241,353-356) of the reference's signed integers
+    (under ``pk``, else the key the vector carries)."""
     n = cv.count
     head = struct.pack("<Q", n)
     if n == 0:
         return head
     dev = cv.device
     lib = _lib.load()
-    mag, neg, exp = cv.export_signed(pk)
+    mag, neg, exp = cv.export_signed(pk) if pk is not None else cv.signed_rows()
     L = int(mag.shape[1])
     s = ctypes.c_void_p(_stream(dev))
     rec_len = torch.empty(n, dtype=torch.int64, device=dev)
@@ -196,16 +197,31 @@ def ciphertext_vector_to_bincode(cv: CiphertextVector, pk: PK) -> bytes:
     return bytes(res)
 
 
-def ciphertext_vector_from_bincode(buf: bytes, pk: PK, device=None) -> Tuple[CiphertextVector, int]:
+# magnitude widths (32-bit words) of the kernels' two geometries: n^2 of <= 1024- and
+# <= 2048-bit keys; a key-less (raw) vector is read at the smaller one that holds its values
+RAW_WIDTHS = (64, 128)
+
+
+def _digit_bits(dig_len: np.ndarray, radix: np.ndarray) -> int:
+    """An upper bound of the bit length of the widest record."""
+    if dig_len.size == 0:
+        return 0
+    return int(np.max(np.ceil(dig_len * np.log2(np.maximum(radix, 2)))))
+
+
+def ciphertext_vector_from_bincode(buf: bytes, pk: Optional[PK] = None, device=None
+                                   ) -> Tuple[CiphertextVector, int]:
     """Parse a ``CiphertextVector`` starting at ``buf[0]``; returns (vector, bytes consumed).
     Radix-16 records and radix-10 records of up to 19 digits (what rug writes) are decoded on
-    the device; any other radix (valid for rug's parser) is parsed on the host.  Raises
-    ``ValueError`` on a malformed record or a value with |c| >= n^2."""
+    the device; any other radix (valid for rug's parser) is parsed on the host.  With ``pk``
+    the vector is converted under that key (ValueError for |c| >= n^2); without, it stays in
+    the reference's key-less signed form (``raw``) until an operation supplies the key.
+    Raises ``ValueError`` on a malformed record."""
     dev = _device(device)
     if len(buf) < 8:
         raise ValueError("bincode: truncated buffer")
     n = struct.unpack_from("<Q", buf, 0)[0]
-    L = pk._key.L2
+    L = pk._key.L2 if pk is not None else RAW_WIDTHS[0]
     if n == 0:
         return CiphertextVector.empty(0, L, dev), 8
     if n > (len(buf) - 8) // MIN_RECORD:  # before sizing anything by an untrusted count
@@ -223,6 +239,10 @@ def ciphertext_vector_from_bincode(buf: bytes, pk: PK, device=None) -> Tuple[Cip
     if st != _lib.FPHE_OK:
         raise ValueError("bincode CiphertextVector: malformed or truncated record")
     used = int(end.value)
+    if pk is None:
+        bits = _digit_bits(dig_len, radix)
+        fits = [w for w in RAW_WIDTHS if 32 * w >= bits]
+        L = fits[0] if fits else RAW_WIDTHS[-1]  # wider than any supported n^2: rejected below
     s = ctypes.c_void_p(_stream(dev))
     dbuf = torch.from_numpy(raw[:used].copy()).to(dev)
     mag = torch.zeros((n, L), dtype=torch.int32, device=dev)
@@ -248,8 +268,13 @@ def ciphertext_vector_from_bincode(buf: bytes, pk: PK, device=None) -> Tuple[Cip
         mag = torch.from_numpy(words.view(np.int32)).to(dev)
     if int(err.item()):
         raise ValueError("bincode CiphertextVector: bad digit or value wider than n^2")
+    negd, expd = torch.from_numpy(neg).to(dev), torch.from_numpy(exp).to(dev)
+    if pk is None:
+        from .paillier import _pad_flat, rows_to_tile_tensor
+        return CiphertextVector(rows_to_tile_tensor(mag), _pad_flat(negd, n), _pad_flat(expd, n), n, None,
+                                raw=True), used
     _check_below(mag, pk.n * pk.n)
-    cv = CiphertextVector.import_signed(pk, mag, torch.from_numpy(neg).to(dev), torch.from_numpy(exp).to(dev))
+    cv = CiphertextVector.import_signed(pk, mag, negd, expd)
     return cv, used
 
 

@@ -208,7 +208,10 @@ fphe_status fphe_sqmul(fphe_ctx* ctx, const uint32_t* Ca, const uint32_t* Cb, co
  * lib.rs:521-791); aligning every per-exponent partial of a fold segment to the segment's
  * minimum exponent and multiplying gives the same integers (the fold is order-independent).
  * Elements in descending-gap order run fastest (a wave pays its largest gap).  gap is a
- * flat int32 array; C arrays tile-major as fphe_add. */
+ * flat int32 array, each 0 <= gap <= 65536 (device memory, so the entry cannot check it: a
+ * negative gap is taken as 0 and a larger one as 65536; the Python layer rejects such gaps,
+ * and no exponent the reference's encoders produce comes near); C arrays tile-major as
+ * fphe_add.  fphe_add likewise caps |exponent gap| at 65536. */
 fphe_status fphe_align(fphe_ctx* ctx, const uint32_t* Ca, const uint8_t* sa, const int32_t* gap, size_t count,
                        uint32_t* Co, uint8_t* so, void* stream);
 

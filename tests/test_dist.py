@@ -8,7 +8,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from fate_amd.dist import WAVE, gather_tiles, shard_bounds
+from fate_amd.dist import WAVE, compact_gathered, gather_tiles, shard_bounds
 
 
 def test_shard_bounds_cover_and_align():
@@ -52,7 +52,7 @@ def _worker(rank, world, port, count, L, q):
             sign[k] = g % 2
             exp[k] = -(g % 7)
         Cg, sg, eg, total = gather_tiles(C, sign, exp, n)
-        ok = total == count
+        ok = total == count and sg.dtype == torch.uint8  # one byte of sign per element on the wire
         for g in range(count):
             ok &= bool(torch.equal(Cg[g // WAVE, :, g % WAVE],
                                    torch.tensor([g * 1000 + j for j in range(L)], dtype=torch.int32)))
@@ -74,6 +74,30 @@ def test_gather_tiles_world2():
     for p in procs:
         p.join(timeout=60)
     assert res == {0: True, 1: True}
+
+
+def test_compact_gathered_ragged_and_whole_tiles():
+    """The receiving side of the all-gather: per-rank padded shards -> one vector in rank
+    order, for whole-tile shards (tile concatenation) and ragged ones (element gather)."""
+    g = torch.Generator().manual_seed(3)
+    L = 3
+    for counts in ([128, 128, 70], [128, 64, 0], [70, 5, 64], [0, 33, 64], [64], [10]):
+        world, nt_max = len(counts), max((c + WAVE - 1) // WAVE for c in counts)
+        full = [torch.randint(0, 1000, (c, L), generator=g, dtype=torch.int32) for c in counts]
+        Cg = torch.zeros((world * nt_max, L, WAVE), dtype=torch.int32)
+        sg = torch.zeros(world * nt_max * WAVE, dtype=torch.uint8)
+        eg = torch.zeros(world * nt_max * WAVE, dtype=torch.int32)
+        for r, rows in enumerate(full):
+            for k in range(rows.shape[0]):
+                Cg[r * nt_max + k // WAVE, :, k % WAVE] = rows[k]
+                sg[r * nt_max * WAVE + k] = (r + k) % 2
+                eg[r * nt_max * WAVE + k] = -(r * 7 + k)
+        C2, s2, e2, tot = compact_gathered(Cg, sg, eg, counts)
+        assert tot == sum(counts)
+        got = C2.permute(0, 2, 1).reshape(-1, L)[:tot]
+        assert torch.equal(got, torch.cat(full))
+        assert s2[:tot].tolist() == [(r + k) % 2 for r, c in enumerate(counts) for k in range(c)]
+        assert e2[:tot].tolist() == [-(r * 7 + k) for r, c in enumerate(counts) for k in range(c)]
 
 
 def _fold_worker(rank, world, port, q):

@@ -240,7 +240,7 @@ def test_random_op_chains_vs_oracle(k1024, seed):
     assert [float(x) for x in got] == [float(x) for x in want]
 
 
-@pytest.mark.parametrize("bits", [512, 770, 1030, 1536])
+@pytest.mark.parametrize("bits", [256, 258, 512, 770, 1026, 1030, 1536])
 def test_other_key_sizes_bit_exact(bits):
     """Even key sizes other than 1024 / 2048 (the reference takes any even size, paillier/
     src/lib.rs:72-87; he_param.key_length is a job parameter) run the 1024- or 2048-bit

@@ -244,13 +244,25 @@ print(json.dumps(out))
 @pytest.mark.parametrize("bits", [1024, 2048])
 def test_ciphertext_and_plaintext_vector_pickle(bits):
     """CiphertextVector / PlaintextVector pickle through the reference's bincode state
-    (paillier.rs:219-226, 395-402), read back under the key of the PK unpickled before them
-    (a PHETensor pickles its PK first) or under fate_amd.paillier.unpickle_key."""
+    (paillier.rs:219-226, 395-402).  A vector's state is the reference's key-less signed
+    integers: unpickled, it stays key-less (raw) -- slices and re-pickles keep it so -- until an
+    operation supplies the key, or is read under fate_amd.paillier.unpickle_key."""
+    import copy
     import pickle
     pk, cv, cs, es = _dev_cts(bits, 300, 7)
     assert cv.__getstate__() == wire.ciphertext_vector_to_bincode(cv, pk) == ct_vec_bytes(cs, es)
     pk2, back = pickle.loads(pickle.dumps((pk, cv)))
-    assert back.to_signed_ints(pk.ns) == (cs, es) and back.n == pk.n
+    assert back.raw and back.n is None and back.to_signed_ints() == (cs, es)
+    assert pickle.loads(pickle.dumps(back)).to_signed_ints() == (cs, es)  # re-pickled without a key
+    sl = back.slice(5, 100)
+    assert sl.raw and sl.to_signed_ints() == (cs[5:105], es[5:105])
+    z = back.add(pk, P.CiphertextVector.zeros(300, pk._key.L2))  # the op gives the key
+    assert not back.raw and back.n == pk.n and back.to_signed_ints(pk.ns) == (cs, es)
+    assert z.to_signed_ints(pk.ns) == (cs, es)  # add(x, literal 1) = x (lib.rs:303-308)
+    assert sl.add(pk, sl).to_signed_ints(pk.ns) == cv.slice(5, 100).add(pk, cv.slice(5, 100)).to_signed_ints(pk.ns)
+    dc = copy.deepcopy(cv)  # a device clone, not a wire round trip
+    assert dc.n == pk.n and not dc.raw and dc.C.data_ptr() != cv.C.data_ptr()
+    assert dc.to_signed_ints(pk.ns) == (cs, es)
     with P.unpickle_key(pk):
         again = pickle.loads(pickle.dumps(cv))
     assert again.to_signed_ints(pk.ns) == (cs, es)
@@ -265,3 +277,21 @@ def test_ciphertext_and_plaintext_vector_pickle(bits):
     assert s.n == pk.n and pickle.loads(pickle.dumps((pk, s)))[1].to_signed_ints(pk.ns) == s.to_signed_ints(pk.ns)
     pv = P.PlaintextVector.from_ints([0, -3, 2**60 + 1], [-14, 2, 0])
     assert pickle.loads(pickle.dumps(pv)).to_ints() == pv.to_ints()
+
+
+@pytest.mark.gpu
+def test_two_keys_never_guessed():
+    """with two keys of one size in a process, a vector pickled under key A and
+    unpickled after PK B must not be read under B.  The state stays key-less and the first
+    operation's key decides: under A it is bit-exact, and decrypting it under B's SK is B's
+    business (no silent conversion happened in between)."""
+    import pickle
+    pkA, cvA, cs, es = _dev_cts(2048, 200, 11)
+    assert any(c < 0 for c in cs)  # negative elements: the case a wrong n^2 would corrupt
+    from fate_amd._keygen import keygen_primes
+    p, q = keygen_primes(2048)
+    skB, pkB, _ = P.keypair_from_primes(p, q)
+    pickle.loads(pickle.dumps(pkB))  # PK B unpickled last in this thread
+    back = pickle.loads(pickle.dumps(cvA))
+    assert back.raw and back.to_signed_ints() == (cs, es)
+    assert back.add(pkA, P.CiphertextVector.zeros(200, 128)).to_signed_ints(pkA.ns) == (cs, es)
