@@ -185,9 +185,10 @@ def cpu_baseline(p: int, q: int, seconds: float = 3.0):
         "usable_cores": d["usable_cores"],
         "cgroup_cpu_max": d["cgroup_cpu_max"],
         "cpu_share": {"cores": d["procs"], "affinity": d["usable_cores"], "cgroup_quota_cpus": d["cgroup_quota_cpus"],
-                      "rule": (f"the GPU box is a 1-GPU slice of an {d['topology']['hw_threads']}-thread host whose "
-                               f"CPU share per GPU is {CPU_SHARE_PER_GPU} (pool rule; no cgroup quota enforces it "
-                               f"when cgroup_quota_cpus is null), so worker pools stay at that share")},
+                      "rule": (f"the GPU box is a 1-GPU slice of a {d['topology']['hw_threads']}-thread host; the worker "
+                               f"pool is the CPU quota of this process's cgroup ({d['cgroup_cpu_max']}) when one is "
+                               f"set, capped at the pool's per-GPU share of {CPU_SHARE_PER_GPU}; the whole host is "
+                               f"projected from it (host_projection)")},
         "topology": d["topology"],
         "smt": d["smt"],
         "host_projection": d["host_projection"],

@@ -1274,6 +1274,7 @@ class PK:
         k = self._key
         n = pv.count
         out = CiphertextVector.empty(n, k.L2, dev)
+        out.n = self.n
         if n == 0:
             return out
         if pv.lp > k.L1:
