@@ -20,6 +20,7 @@ FPHE_ERR_ARG = 1
 FPHE_ERR_HIP = 2
 FPHE_ERR_NO_SK = 3
 FPHE_ERR_KEY = 4
+FPHE_ERR_RANGE = 5
 
 EF_ENCODE_NONFINITE = 0x01
 EF_DECODE_CORRUPTED = 0x02
@@ -27,6 +28,7 @@ EF_DECODE_OVERFLOW = 0x04
 EF_MUL_INVALID_PT = 0x08
 EF_NOT_INVERTIBLE = 0x10
 EF_DECODE_I128 = 0x20
+EF_EXP_RANGE = 0x40
 
 # every symbol declared in include/fate_phe.h
 EXPORTED_SYMBOLS = (
@@ -34,7 +36,7 @@ EXPORTED_SYMBOLS = (
     "fphe_encode_f32", "fphe_encode_f64", "fphe_decode_f32", "fphe_decode_f64",
     "fphe_encode_i64", "fphe_decode_i64", "fphe_decode_i32", "fphe_pack_f64", "fphe_unpack_f64",
     "fphe_encrypt", "fphe_encrypt_crt", "fphe_decrypt", "fphe_add", "fphe_add_ordered", "fphe_mul", "fphe_neg", "fphe_sqmul", "fphe_align",
-    "fphe_fold", "fphe_permute", "fphe_export_signed", "fphe_import_signed",
+    "fphe_fold", "fphe_fold_segments", "fphe_permute", "fphe_export_signed", "fphe_import_signed",
     "fphe_wire_lengths", "fphe_wire_encode", "fphe_wire_scan", "fphe_wire_decode", "fphe_chacha20_blocks",
 )
 
@@ -110,6 +112,9 @@ def load() -> ctypes.CDLL:
         lib.fphe_align.restype = st
         lib.fphe_fold.argtypes = [vp, vp, vp, vp, vp, vp, vp, ctypes.c_size_t, vp, vp, vp, vp]
         lib.fphe_fold.restype = st
+        lib.fphe_fold_segments.argtypes = [vp, vp, vp, vp, ctypes.c_size_t, vp, vp, ctypes.c_size_t, ctypes.c_size_t,
+                                           vp, vp, vp, vp, vp, vp]
+        lib.fphe_fold_segments.restype = st
         lib.fphe_permute.argtypes = [vp, vp, vp, ctypes.c_uint32, vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int,
                                      vp, vp, vp, vp]
         lib.fphe_permute.restype = st

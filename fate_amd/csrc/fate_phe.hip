@@ -485,6 +485,9 @@ __global__ __launch_bounds__(256) void k_decode_f64(KeyArgs K, const u32* __rest
 
 #include "codec_dev.h"
 #include "kernels27.h"
+namespace {
+#include "group_dev.h"
+}  // namespace
 
 // ======================================================================================
 // host side: context + C ABI
@@ -708,12 +711,235 @@ fphe_status launch_fold27(fphe_ctx* c, const uint32_t* Src, const uint8_t* ssign
                           const int64_t* ord, const int64_t* cstart, const int32_t* clen, size_t nchunks,
                           uint32_t* Co, uint8_t* so, int32_t* eo, hipStream_t s) {
   constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = rad_ll(TPI) * TPI;
-  auto kern = KS<TPI>::template fold<L>();
+  auto kern = KS<TPI>::template fold<L, int64_t, false>();
   const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
   set_lds(kern, lds);
   const unsigned grid = occ_grid(c, kern, lds, (nchunks + E - 1) / E, "fold27");
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, Src, ssign, sexp, ord, cstart, clen, nchunks,
-                     c->K.FR_27, Co, so, eo, (u32)NL);
+                     (const int32_t*)nullptr, c->K.FR_27, Co, so, eo, (u32)NL);
+  return hip_ok(hipGetLastError());
+}
+
+// ---- segmented fold with device grouping (fphe_fold_segments) --------------------------------
+// Stream-ordered scratch of one call: freed (hipFreeAsync) on the call's stream at the end.
+struct CallBufs {
+  hipStream_t s;
+  std::vector<void*> ptrs;
+  bool ok = true;
+  explicit CallBufs(hipStream_t st) : s(st) {}
+  template <class T>
+  T* get(size_t n) {
+    void* p = nullptr;
+    if (hipMallocAsync(&p, (n ? n : 1) * sizeof(T), s) != hipSuccess) {
+      ok = false;
+      return nullptr;
+    }
+    ptrs.push_back(p);
+    return (T*)p;
+  }
+  ~CallBufs() {
+    for (void* p : ptrs) (void)hipFreeAsync(p, s);
+  }
+};
+
+constexpr size_t kMaxFoldKeys = (size_t)1 << 25;  // (segment, exponent) buckets per call
+
+// exclusive scan of n int32 on the device (3 launches); the total lands in *total if given
+fphe_status dev_scan(const fphe_ctx* c, const int32_t* in, size_t n, int32_t* out, int32_t* total, CallBufs& B) {
+  const size_t nb = (n + kScanTile - 1) / kScanTile;
+  int32_t* bsum = B.get<int32_t>(nb);
+  if (!B.ok) return FPHE_ERR_HIP;
+  hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)(nb ? nb : 1)), dim3(kGrBlock), 0, B.s, in, n, out, bsum);
+  hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(kGrBlock), 0, B.s, bsum, nb, total);
+  hipLaunchKernelGGL(k_scan_add, dim3((unsigned)(nb ? nb : 1)), dim3(kGrBlock), 0, B.s, out, n, bsum);
+  (void)c;
+  return hip_ok(hipGetLastError());
+}
+
+int32_t fold_klen(size_t n) {  // chunk length: fill ~32K wave slots, 8..64 terms (kFoldMax)
+  size_t k = (n + 32767) / 32768;
+  return (int32_t)(k < 8 ? 8 : (k > (size_t)kFoldMax ? (size_t)kFoldMax : k));
+}
+
+// A fold level's input: n items (element-major rows + sign + exp), grouped by key in
+// contiguous runs: key k's items at [off[k], off[k] + cnt[k]) of the item order (ord, or the
+// items themselves when ord is null).
+struct FoldLevel {
+  const u32* rows;
+  const u8* sign;
+  const int32_t* exp;
+  const int32_t* ord;
+  const int32_t* cnt;
+  const int32_t* off;
+  size_t nkeys;
+  int32_t maxcnt;  // largest run
+};
+struct FoldOut {
+  u32* rows;
+  u8* sign;
+  int32_t* exp;
+  int32_t* key;  // key of each output partial (ascending)
+  int32_t* cnt;  // per key: partials produced
+  int32_t* off;  // per key: first partial
+  size_t n;      // partials
+  int32_t maxcnt;
+};
+
+template <int L>
+fphe_status fold_level(fphe_ctx* c, const FoldLevel& in, size_t nitems, FoldOut& out, CallBufs& B) {
+  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = rad_ll(TPI) * TPI;
+  hipStream_t s = B.s;
+  const int32_t k = fold_klen(nitems);
+  int32_t* nch = B.get<int32_t>(in.nkeys);
+  int32_t* choff = B.get<int32_t>(in.nkeys);
+  int32_t* hdr = B.get<int32_t>(4);
+  if (!B.ok) return FPHE_ERR_HIP;
+  if (hipMemsetAsync(hdr, 0, 4 * sizeof(int32_t), s) != hipSuccess) return FPHE_ERR_HIP;
+  hipLaunchKernelGGL(k_gr_nchunks, dim3(gr_grid(in.nkeys, c->cus)), dim3(kGrBlock), 0, s, in.cnt, in.nkeys, k, nch, hdr);
+  if (dev_scan(c, nch, in.nkeys, choff, hdr + 2, B) != FPHE_OK) return FPHE_ERR_HIP;
+  int32_t h[4];
+  if (hipMemcpyAsync(h, hdr, sizeof(h), hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+    return FPHE_ERR_HIP;
+  const size_t nchk = (size_t)h[2];
+  int32_t* cstart = B.get<int32_t>(nchk);
+  int32_t* clen = B.get<int32_t>(nchk);
+  out.key = B.get<int32_t>(nchk);
+  out.rows = B.get<u32>(nchk * L);
+  out.sign = B.get<u8>(nchk);
+  out.exp = B.get<int32_t>(nchk);
+  if (!B.ok) return FPHE_ERR_HIP;
+  hipLaunchKernelGGL(k_gr_chunks, dim3(gr_grid(in.nkeys, c->cus)), dim3(kGrBlock), 0, s, in.cnt, in.off, choff, in.nkeys,
+                     k, cstart, clen, out.key);
+  auto kern = KS<TPI>::template fold<L, int32_t, true>();
+  const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
+  set_lds(kern, lds);
+  const unsigned grid = occ_grid(c, kern, lds, (nchk + E - 1) / E, "fold_segments");
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, in.rows, in.sign, in.exp, in.ord, cstart, clen,
+                     nchk, (const int32_t*)nullptr, c->K.FR_27, out.rows, out.sign, out.exp, (u32)NL);
+  out.cnt = nch;
+  out.off = choff;
+  out.n = nchk;
+  out.maxcnt = (in.maxcnt + k - 1) / k;
+  return hip_ok(hipGetLastError());
+}
+
+// fold every key's run down to one partial (levels of chunked products)
+template <int L>
+fphe_status fold_runs(fphe_ctx* c, FoldLevel lv, size_t nitems, FoldOut& out, CallBufs& B) {
+  for (;;) {
+    if (fold_level<L>(c, lv, nitems, out, B) != FPHE_OK) return FPHE_ERR_HIP;
+    if (out.maxcnt <= 1) return FPHE_OK;
+    lv = FoldLevel{out.rows, out.sign, out.exp, nullptr, out.cnt, out.off, lv.nkeys, out.maxcnt};
+    nitems = out.n;
+  }
+}
+
+template <int L>
+fphe_status launch_fold_segments(fphe_ctx* c, const u32* Src, const u8* ssign, const int32_t* sexp, size_t nsrc,
+                                 const int32_t* idx, const int32_t* seg, size_t T, size_t nseg, u32* Co, u8* so,
+                                 int32_t* eo, u8* present, int32_t* err, hipStream_t s) {
+  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = rad_ll(TPI) * TPI;
+  CallBufs B(s);
+  const unsigned g0 = gr_grid(nseg * FPHE_WAVE, c->cus);
+  hipLaunchKernelGGL(k_gr_init_out<L>, dim3(g0), dim3(kGrBlock), 0, s, nseg, Co, so, eo, present);
+  if (T == 0) return hip_ok(hipGetLastError());
+  // 1. exponent range (one small read back: it sizes the key space)
+  int32_t* mm = B.get<int32_t>(4);
+  if (!B.ok) return FPHE_ERR_HIP;
+  const int32_t mm0[4] = {kI32Max, kI32Min, 0, 0};
+  if (hipMemcpyAsync(mm, mm0, sizeof(mm0), hipMemcpyHostToDevice, s) != hipSuccess) return FPHE_ERR_HIP;
+  hipLaunchKernelGGL(k_gr_minmax, dim3(gr_grid(T, c->cus)), dim3(kGrBlock), 0, s, idx, seg, sexp, T, nsrc, nseg, mm);
+  int32_t h[4];
+  if (hipMemcpyAsync(h, mm, sizeof(h), hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+    return FPHE_ERR_HIP;
+  if (h[2]) return FPHE_ERR_ARG;  // an index or segment out of range
+  const int64_t NE = (int64_t)h[1] - h[0] + 1;
+  if (NE < 1 || (size_t)NE * nseg > kMaxFoldKeys) return FPHE_ERR_RANGE;
+  const size_t nkeys = (size_t)NE * nseg;
+  // 2. element-major copy of the source (the fold gathers whole rows)
+  u32* rows = B.get<u32>(nsrc * L);
+  int32_t* keys = B.get<int32_t>(T);
+  int32_t* cnt = B.get<int32_t>(nkeys);
+  int32_t* off = B.get<int32_t>(nkeys);
+  int32_t* fill = B.get<int32_t>(nkeys);
+  int32_t* last = B.get<int32_t>(nseg);
+  int32_t* ord = B.get<int32_t>(T);
+  if (!B.ok) return FPHE_ERR_HIP;
+  hipLaunchKernelGGL(k_tiles_to_rows<L>, dim3((unsigned)std::min<size_t>(ntiles_of(nsrc), (size_t)c->cus * 8)),
+                     dim3(kGrBlock), 0, s, Src, nsrc, rows);
+  // 3. keys, counts, counting sort
+  if (hipMemsetAsync(cnt, 0, nkeys * 4, s) != hipSuccess || hipMemsetAsync(fill, 0, nkeys * 4, s) != hipSuccess ||
+      hipMemsetAsync(last, 0xff, nseg * 4, s) != hipSuccess)
+    return FPHE_ERR_HIP;
+  hipLaunchKernelGGL(k_gr_keys, dim3(gr_grid(T, c->cus)), dim3(kGrBlock), 0, s, idx, seg, sexp, T, h[0], (int32_t)NE,
+                     keys, cnt, last);
+  if (dev_scan(c, cnt, nkeys, off, nullptr, B) != FPHE_OK) return FPHE_ERR_HIP;
+  hipLaunchKernelGGL(k_gr_scatter, dim3(gr_grid(T, c->cus)), dim3(kGrBlock), 0, s, keys, idx, T, off, fill, ord);
+  // 4. fold every (segment, exponent) run to one partial
+  FoldOut P{};
+  if (fold_runs<L>(c, FoldLevel{rows, ssign, sexp, ord, cnt, off, nkeys, (int32_t)T}, T, P, B) != FPHE_OK)
+    return FPHE_ERR_HIP;
+  // 5. merge each segment's per-exponent partials: align to the segment's least exponent, fold
+  if (NE > 1) {
+    int32_t* segmin = B.get<int32_t>(nseg);
+    u8* lit = B.get<u8>(P.n);
+    int32_t* gap = B.get<int32_t>(P.n);
+    int32_t* skey = B.get<int32_t>(P.n);
+    int32_t* scnt = B.get<int32_t>(nseg);
+    int32_t* soff = B.get<int32_t>(nseg);
+    int32_t* gh = B.get<int32_t>(2);
+    int32_t* np_dev = B.get<int32_t>(1);
+    if (!B.ok) return FPHE_ERR_HIP;
+    const int32_t npi = (int32_t)P.n;
+    if (hipMemsetD32Async((hipDeviceptr_t)segmin, kI32Max, nseg, s) != hipSuccess ||
+        hipMemsetAsync(scnt, 0, nseg * 4, s) != hipSuccess || hipMemsetAsync(gh, 0, 8, s) != hipSuccess ||
+        hipMemcpyAsync(np_dev, &npi, 4, hipMemcpyHostToDevice, s) != hipSuccess)
+      return FPHE_ERR_HIP;
+    const unsigned gp = gr_grid(P.n, c->cus);
+    hipLaunchKernelGGL(k_gr_segmin<L>, dim3(gp), dim3(kGrBlock), 0, s, P.rows, P.sign, P.exp, P.key, np_dev,
+                       (int32_t)NE, segmin, lit);
+    hipLaunchKernelGGL(k_gr_gaps, dim3(gp), dim3(kGrBlock), 0, s, P.exp, P.key, lit, np_dev, (int32_t)NE, segmin, gap,
+                       skey, scnt, gh, err);
+    if (hipMemcpyAsync(h, gh, 8, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+      return FPHE_ERR_HIP;
+    const int32_t gmax = h[0];
+    if (gmax > 0) {
+      // partials in descending-gap order (counting sort on gmax - gap), then the alignment
+      const size_t ng = (size_t)gmax + 1;
+      int32_t* gk = B.get<int32_t>(P.n);
+      int32_t* gc = B.get<int32_t>(ng);
+      int32_t* go = B.get<int32_t>(ng);
+      int32_t* gf = B.get<int32_t>(ng);
+      int32_t* gord = B.get<int32_t>(P.n);
+      u32* tile_ctr = B.get<u32>(1);
+      if (!B.ok) return FPHE_ERR_HIP;
+      if (hipMemsetAsync(gc, 0, ng * 4, s) != hipSuccess || hipMemsetAsync(gf, 0, ng * 4, s) != hipSuccess ||
+          hipMemsetAsync(tile_ctr, 0, 4, s) != hipSuccess)
+        return FPHE_ERR_HIP;
+      hipLaunchKernelGGL(k_gr_gapkeys, dim3(gp), dim3(kGrBlock), 0, s, gap, P.n, gmax, gk, gc);
+      if (dev_scan(c, gc, ng, go, nullptr, B) != FPHE_OK) return FPHE_ERR_HIP;
+      hipLaunchKernelGGL(k_gr_scatter, dim3(gp), dim3(kGrBlock), 0, s, gk, (const int32_t*)nullptr, P.n, go, gf, gord);
+      auto ka = KS<TPI>::template align_rows<L>();
+      const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
+      set_lds(ka, lds);
+      const unsigned ga = occ_grid(c, ka, lds, (P.n + E - 1) / E, "align_rows");
+      hipLaunchKernelGGL(ka, dim3(ga), dim3(kBlock), lds, s, c->K, P.rows, P.sign, gap, gord, np_dev, tile_ctr,
+                         (u32)NL);
+    }
+    // the partials are in (segment, exponent) order: contiguous per segment
+    if (dev_scan(c, scnt, nseg, soff, nullptr, B) != FPHE_OK) return FPHE_ERR_HIP;
+    FoldOut Q{};
+    if (fold_runs<L>(c, FoldLevel{P.rows, P.sign, P.exp, nullptr, scnt, soff, nseg, (int32_t)NE}, P.n, Q, B) != FPHE_OK)
+      return FPHE_ERR_HIP;
+    P = Q;
+  }
+  // 6. scatter to the output segments (keys are segment ids here)
+  int32_t* nfin = B.get<int32_t>(1);
+  if (!B.ok) return FPHE_ERR_HIP;
+  const int32_t nf = (int32_t)P.n;
+  if (hipMemcpyAsync(nfin, &nf, 4, hipMemcpyHostToDevice, s) != hipSuccess) return FPHE_ERR_HIP;
+  hipLaunchKernelGGL(k_gr_final<L>, dim3(gr_grid(P.n * 64, c->cus)), dim3(kGrBlock), 0, s, P.rows, P.sign, P.exp, P.key,
+                     nfin, last, idx, sexp, Co, so, eo, present);
   return hip_ok(hipGetLastError());
 }
 
@@ -1458,6 +1684,24 @@ fphe_status fphe_fold(fphe_ctx* c, const uint32_t* Src, const uint8_t* ssign, co
   if (c->L2 == 128)
     return launch_fold27<128>(c, Src, ssign, sexp, ord, cstart, clen, nchunks, Co, so, eo, (hipStream_t)stream);
   return launch_fold27<64>(c, Src, ssign, sexp, ord, cstart, clen, nchunks, Co, so, eo, (hipStream_t)stream);
+}
+
+
+fphe_status fphe_fold_segments(fphe_ctx* c, const uint32_t* Src, const uint8_t* ssign, const int32_t* sexp,
+                               size_t nsrc, const int32_t* idx, const int32_t* seg, size_t nterms, size_t nseg,
+                               uint32_t* Co, uint8_t* so, int32_t* eo, uint8_t* present, int32_t* err, void* stream) {
+  if (!c) return FPHE_ERR_ARG;
+  if (nseg == 0) return nterms ? FPHE_ERR_ARG : FPHE_OK;
+  if (!Co || !so || !eo || !err || (nterms && (!Src || !ssign || !sexp || !seg))) return FPHE_ERR_ARG;
+  if (nterms >= (1ull << 31) || nsrc >= (1ull << 31) || nseg >= (1ull << 31)) return FPHE_ERR_ARG;
+  if (nterms && !idx && nsrc < nterms) return FPHE_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DevGuard g(c->device);
+  if (c->L2 == 128)
+    return launch_fold_segments<128>(c, Src, ssign, sexp, nsrc, idx, seg, nterms, nseg, Co, so, eo, present, err,
+                                     (hipStream_t)stream);
+  return launch_fold_segments<64>(c, Src, ssign, sexp, nsrc, idx, seg, nterms, nseg, Co, so, eo, present, err,
+                                  (hipStream_t)stream);
 }
 
 

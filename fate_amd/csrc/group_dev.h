@@ -1,0 +1,339 @@
+// Device grouping for the segmented ciphertext folds (fphe_fold_segments): the integer
+// plumbing around the Montgomery fold kernels -- term keys, a counting sort of the terms by
+// (segment, exponent), chunk tables, the per-segment exponent merge bookkeeping and the
+// final scatter.  All HBM-bound byte/int work: one thread per term, key or partial, grid
+// stride loops, atomics on 32-bit counters.  Included by fate_phe.hip inside its anonymous
+// namespace (after set_err / kBlock).
+//
+// Reference: the sequential Ciphertext::add folds of iupdate / iupdate_with_masks /
+// intervals_sum_with_step / matmul (fixedpoint_paillier/src/lib.rs:724-791, 861-908); the fold
+// is order independent, which is what lets the terms be regrouped.
+
+#pragma once
+
+constexpr int kGrBlock = 256;
+constexpr int32_t kI32Max = 0x7fffffff;
+constexpr int32_t kI32Min = -0x7fffffff - 1;
+
+// grid size for a one-thread-per-item integer kernel: enough blocks to fill the chip, no more
+inline unsigned gr_grid(size_t n, int cus) {
+  size_t g = (n + kGrBlock - 1) / kGrBlock;
+  const size_t cap = (size_t)cus * 8;
+  if (g > cap) g = cap;
+  return (unsigned)(g ? g : 1);
+}
+
+// --- pass 1: exponent range of the terms and index bounds -------------------------------------
+// mm[0] = min exponent, mm[1] = max exponent over the terms' sources (INT_MAX / INT_MIN when no
+// term), mm[2] |= 1 on an index outside [0, nsrc) or a segment outside [0, nseg).
+__global__ __launch_bounds__(kGrBlock) void k_gr_minmax(const int32_t* __restrict__ idx, const int32_t* __restrict__ seg,
+                                                        const int32_t* __restrict__ sexp, size_t T, size_t nsrc,
+                                                        size_t nseg, int32_t* __restrict__ mm) {
+  int32_t lo = kI32Max, hi = kI32Min;
+  int32_t bad = 0;
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < T; t += (size_t)gridDim.x * blockDim.x) {
+    const int32_t s = idx ? idx[t] : (int32_t)t;
+    const int32_t g = seg[t];
+    if (s < 0 || (size_t)s >= nsrc || g < 0 || (size_t)g >= nseg) {
+      bad = 1;
+      continue;
+    }
+    const int32_t e = sexp[s];
+    lo = e < lo ? e : lo;
+    hi = e > hi ? e : hi;
+  }
+  __shared__ int32_t slo[kGrBlock / 64], shi[kGrBlock / 64], sbad[kGrBlock / 64];
+  // wave reduction, then one atomic per block
+  for (int o = 32; o > 0; o >>= 1) {
+    const int32_t l2 = __shfl_xor(lo, o), h2 = __shfl_xor(hi, o), b2 = __shfl_xor(bad, o);
+    lo = l2 < lo ? l2 : lo;
+    hi = h2 > hi ? h2 : hi;
+    bad |= b2;
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    slo[w] = lo;
+    shi[w] = hi;
+    sbad[w] = bad;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < kGrBlock / 64; ++i) {
+      lo = slo[i] < lo ? slo[i] : lo;
+      hi = shi[i] > hi ? shi[i] : hi;
+      bad |= sbad[i];
+    }
+    atomicMin(&mm[0], lo);
+    atomicMax(&mm[1], hi);
+    if (bad) atomicOr(&mm[2], 1);
+  }
+}
+
+// --- pass 2: keys and counts ----------------------------------------------------------------
+// key = seg * NE + (exp - emin); cnt[key] += 1; last[seg] = max term position (the reference's
+// sequential fold ends on the segment's last term: the exponent of an all-literal-1 segment).
+__global__ __launch_bounds__(kGrBlock) void k_gr_keys(const int32_t* __restrict__ idx, const int32_t* __restrict__ seg,
+                                                      const int32_t* __restrict__ sexp, size_t T, int32_t emin, int32_t NE,
+                                                      int32_t* __restrict__ keys, int32_t* __restrict__ cnt,
+                                                      int32_t* __restrict__ last) {
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < T; t += (size_t)gridDim.x * blockDim.x) {
+    const int32_t s = idx ? idx[t] : (int32_t)t;
+    const int32_t g = seg[t];
+    const int32_t k = g * NE + (sexp[s] - emin);
+    keys[t] = k;
+    atomicAdd(&cnt[k], 1);
+    atomicMax(&last[g], (int32_t)t);
+  }
+}
+
+// nch[key] = ceil(cnt[key] / klen); stats[0] = max cnt, stats[1] = non-empty keys
+__global__ __launch_bounds__(kGrBlock) void k_gr_nchunks(const int32_t* __restrict__ cnt, size_t nkeys, int32_t klen,
+                                                         int32_t* __restrict__ nch, int32_t* __restrict__ stats) {
+  int32_t mx = 0, nz = 0;
+  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < nkeys; k += (size_t)gridDim.x * blockDim.x) {
+    const int32_t c = cnt[k];
+    nch[k] = (c + klen - 1) / klen;
+    mx = c > mx ? c : mx;
+    nz += c > 0;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const int32_t m2 = __shfl_xor(mx, o);
+    mx = m2 > mx ? m2 : mx;
+    nz += __shfl_xor(nz, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMax(&stats[0], mx);
+    atomicAdd(&stats[1], nz);
+  }
+}
+
+// --- exclusive scan of int32 counts (3 passes; n up to 2^31 - 1 total) -------------------------
+constexpr int kScanItems = 8;  // per thread
+constexpr int kScanTile = kGrBlock * kScanItems;
+
+__device__ __forceinline__ int32_t block_excl_scan(int32_t v, int32_t* total) {
+  __shared__ int32_t ws[kGrBlock / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int32_t x = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int32_t y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) ws[w] = x;
+  __syncthreads();
+  int32_t base = 0, tot = 0;
+  for (int i = 0; i < kGrBlock / 64; ++i) {
+    if (i < w) base += ws[i];
+    tot += ws[i];
+  }
+  __syncthreads();
+  *total = tot;
+  return base + x - v;
+}
+
+// out[i] = exclusive prefix within the tile; bsum[tile] = tile total
+__global__ __launch_bounds__(kGrBlock) void k_scan_tiles(const int32_t* __restrict__ in, size_t n,
+                                                         int32_t* __restrict__ out, int32_t* __restrict__ bsum) {
+  const size_t t0 = (size_t)blockIdx.x * kScanTile;
+  int32_t v[kScanItems], s = 0;
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i) {
+    const size_t j = t0 + (size_t)threadIdx.x * kScanItems + i;
+    v[i] = j < n ? in[j] : 0;
+    s += v[i];
+  }
+  int32_t tot;
+  int32_t run = block_excl_scan(s, &tot);
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i) {
+    const size_t j = t0 + (size_t)threadIdx.x * kScanItems + i;
+    if (j < n) out[j] = run;
+    run += v[i];
+  }
+  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+
+// exclusive scan of the tile totals in one block (nb tiles, looping); total -> *total
+__global__ __launch_bounds__(kGrBlock) void k_scan_sums(int32_t* __restrict__ bsum, size_t nb, int32_t* __restrict__ total) {
+  int32_t carry = 0;
+  for (size_t b0 = 0; b0 < nb; b0 += kGrBlock) {
+    const size_t j = b0 + threadIdx.x;
+    const int32_t v = j < nb ? bsum[j] : 0;
+    int32_t tot;
+    const int32_t ex = block_excl_scan(v, &tot);
+    if (j < nb) bsum[j] = carry + ex;
+    carry += tot;
+  }
+  if (threadIdx.x == 0 && total) *total = carry;
+}
+
+__global__ __launch_bounds__(kGrBlock) void k_scan_add(int32_t* __restrict__ out, size_t n, const int32_t* __restrict__ bsum) {
+  const size_t t0 = (size_t)blockIdx.x * kScanTile;
+  const int32_t add = bsum[blockIdx.x];
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i) {
+    const size_t j = t0 + (size_t)i * kGrBlock + threadIdx.x;
+    if (j < n) out[j] += add;
+  }
+}
+
+// --- pass 3: counting-sort scatter ------------------------------------------------------------
+// ord[off[key] + rank] = source index of the term (rank by an atomic cursor: the order within a
+// key is arbitrary, the fold does not depend on it)
+__global__ __launch_bounds__(kGrBlock) void k_gr_scatter(const int32_t* __restrict__ keys, const int32_t* __restrict__ idx,
+                                                         size_t T, const int32_t* __restrict__ off,
+                                                         int32_t* __restrict__ fill, int32_t* __restrict__ ord) {
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < T; t += (size_t)gridDim.x * blockDim.x) {
+    const int32_t k = keys[t];
+    const int32_t pos = off[k] + atomicAdd(&fill[k], 1);
+    ord[pos] = idx ? idx[t] : (int32_t)t;
+  }
+}
+
+// --- chunk tables: key k's items [off[k], off[k] + cnt[k]) in chunks of klen ----------------------
+__global__ __launch_bounds__(kGrBlock) void k_gr_chunks(const int32_t* __restrict__ cnt, const int32_t* __restrict__ off,
+                                                        const int32_t* __restrict__ choff, size_t nkeys, int32_t klen,
+                                                        int32_t* __restrict__ cstart, int32_t* __restrict__ clen,
+                                                        int32_t* __restrict__ ckey) {
+  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < nkeys; k += (size_t)gridDim.x * blockDim.x) {
+    const int32_t c = cnt[k];
+    const int32_t b = off[k], cb = choff[k];
+    for (int32_t i = 0; i * klen < c; ++i) {
+      cstart[cb + i] = b + i * klen;
+      const int32_t r = c - i * klen;
+      clen[cb + i] = r < klen ? r : klen;
+      ckey[cb + i] = (int32_t)k;
+    }
+  }
+}
+
+// --- exponent merge ---------------------------------------------------------------------------------
+// Per final (segment, exponent) partial p (element-major rows, L words): literal-1 test (the
+// reference's zero: signed integer exactly 1) and the segment's least non-literal exponent.
+template <int L>
+__global__ __launch_bounds__(kGrBlock) void k_gr_segmin(const u32* __restrict__ rows, const u8* __restrict__ sign,
+                                                        const int32_t* __restrict__ exp, const int32_t* __restrict__ pkey,
+                                                        const int32_t* __restrict__ np_dev, int32_t NE,
+                                                        int32_t* __restrict__ segmin, u8* __restrict__ lit) {
+  const int32_t np = *np_dev;
+  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < (size_t)np; p += (size_t)gridDim.x * blockDim.x) {
+    const u32* r = rows + p * L;
+    u32 acc = r[0] ^ 1u;
+    for (int j = 1; j < L; ++j) acc |= r[j];
+    const bool one = acc == 0 && sign[p] == 0;
+    lit[p] = one ? 1 : 0;
+    if (!one) atomicMin(&segmin[pkey[p] / NE], exp[p]);
+  }
+}
+
+// gap[p] = exp - segmin (0 for literal partials and all-literal segments), exp[p] = segmin (the
+// exponent every partial of the segment is aligned to), nseg-keys for the next fold, counts;
+// gap beyond kMaxGap -> err (fphe_align's contract).  gmax = the largest gap (device).
+__global__ __launch_bounds__(kGrBlock) void k_gr_gaps(int32_t* __restrict__ exp, const int32_t* __restrict__ pkey,
+                                                      const u8* __restrict__ lit, const int32_t* __restrict__ np_dev,
+                                                      int32_t NE, const int32_t* __restrict__ segmin,
+                                                      int32_t* __restrict__ gap, int32_t* __restrict__ skey,
+                                                      int32_t* __restrict__ scnt, int32_t* __restrict__ gmax,
+                                                      int32_t* __restrict__ err) {
+  const int32_t np = *np_dev;
+  u32 ef = 0;
+  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < (size_t)np; p += (size_t)gridDim.x * blockDim.x) {
+    const int32_t s = pkey[p] / NE;
+    const int32_t m = segmin[s];
+    int32_t d = 0;
+    if (m != kI32Max) {
+      if (!lit[p]) {
+        const long long dd = (long long)exp[p] - m;
+        d = dd > kMaxGap ? kMaxGap : (int32_t)dd;
+        if (dd > kMaxGap) ef |= FPHE_EF_EXP_RANGE;
+      }
+      exp[p] = m;
+    }
+    gap[p] = d;
+    skey[p] = s;
+    atomicAdd(&scnt[s], 1);
+    if (d) atomicMax(gmax, d);
+  }
+  set_err(err, ef);
+}
+
+// counting-sort keys for the descending-gap order of the alignment: key = gmax - gap
+__global__ __launch_bounds__(kGrBlock) void k_gr_gapkeys(const int32_t* __restrict__ gap, size_t n, int32_t gmax,
+                                                         int32_t* __restrict__ keys, int32_t* __restrict__ cnt) {
+  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x) {
+    const int32_t k = gmax - gap[p];
+    keys[p] = k;
+    atomicAdd(&cnt[k], 1);
+  }
+}
+
+// --- element-major <-> tile-major ------------------------------------------------------------------
+// One block per 64-element tile: [L][64] words (coalesced 256-B rows) -> 64 rows of L words
+// (coalesced), through LDS with a 65-word row pitch (no bank conflicts on the transposed read).
+template <int L>
+__global__ __launch_bounds__(kGrBlock) void k_tiles_to_rows(const u32* __restrict__ C, size_t count, u32* __restrict__ rows) {
+  __shared__ u32 t[L][FPHE_WAVE + 1];
+  const size_t ntiles = (count + FPHE_WAVE - 1) / FPHE_WAVE;
+  for (size_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const u32* src = C + tile * L * FPHE_WAVE;
+    for (int i = threadIdx.x; i < L * FPHE_WAVE; i += kGrBlock) t[i >> 6][i & 63] = src[i];
+    __syncthreads();
+    const size_t e0 = tile * FPHE_WAVE;
+    const int ne = count - e0 < (size_t)FPHE_WAVE ? (int)(count - e0) : FPHE_WAVE;
+    for (int i = threadIdx.x; i < ne * L; i += kGrBlock) rows[(e0 + i / L) * L + i % L] = t[i % L][i / L];
+    __syncthreads();
+  }
+}
+
+// Final scatter: out[seg] (tile-major) for every segment: the segment's folded partial, or the
+// literal 1 (exp 0) for a segment without terms.  A literal-1 result takes the exponent of the
+// segment's last term (the reference's sequential fold ends on it, lib.rs:303-308).
+template <int L>
+__global__ __launch_bounds__(kGrBlock) void k_gr_init_out(size_t nseg, u32* __restrict__ Co, u8* __restrict__ so,
+                                                          int32_t* __restrict__ eo, u8* __restrict__ present) {
+  const size_t nt = (nseg + FPHE_WAVE - 1) / FPHE_WAVE;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nt * L * FPHE_WAVE; i += (size_t)gridDim.x * blockDim.x) {
+    const size_t w = (i >> 6) % L;
+    Co[i] = w == 0 ? 1u : 0u;
+  }
+  for (size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x; s < nt * FPHE_WAVE; s += (size_t)gridDim.x * blockDim.x) {
+    so[s] = 0;
+    eo[s] = 0;
+    if (present) present[s] = 0;
+  }
+}
+
+template <int L>
+__global__ __launch_bounds__(kGrBlock) void k_gr_final(const u32* __restrict__ rows, const u8* __restrict__ sign,
+                                                       const int32_t* __restrict__ exp, const int32_t* __restrict__ pkey,
+                                                       const int32_t* __restrict__ np_dev,
+                                                       const int32_t* __restrict__ last, const int32_t* __restrict__ idx,
+                                                       const int32_t* __restrict__ sexp, u32* __restrict__ Co,
+                                                       u8* __restrict__ so, int32_t* __restrict__ eo,
+                                                       u8* __restrict__ present) {
+  const int32_t np = *np_dev;
+  // one wave per partial: lanes copy words, lane 0 the per-element fields
+  const size_t lane = threadIdx.x & 63;
+  const size_t w0 = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6, nwv = ((size_t)gridDim.x * blockDim.x) >> 6;
+  for (size_t p = w0; p < (size_t)np; p += nwv) {
+    const u32* r = rows + p * L;
+    const int32_t s = pkey[p];
+    u32 acc = 0;
+    for (int j = (int)lane; j < L; j += 64) {
+      const u32 v = r[j];
+      acc |= j == 0 ? (v ^ 1u) : v;
+      Co[(((size_t)s >> 6) * L + j) * FPHE_WAVE + (s & 63)] = v;
+    }
+    const bool one = __ballot(acc != 0) == 0 && sign[p] == 0;
+    if (lane == 0) {
+      so[s] = sign[p];
+      int32_t e = exp[p];
+      if (one) {
+        const int32_t t = last[s];
+        e = sexp[idx ? idx[t] : t];
+      }
+      eo[s] = e;
+      if (present) present[s] = 1;
+    }
+  }
+}

@@ -126,17 +126,13 @@ def fold_partials(pk, parts, nparts: int, m: int):
     r's slot j at r * m + j): out[j] = add(... add(parts[j], parts[m + j]) ...), with the
     device segmented fold (the same path as iupdate), bit-exact with the sequential ct-add
     chain by the order independence of the fold."""
-    from .paillier import CiphertextVector, _fold_segments
+    from .paillier import _fold_to_segments
 
     dev = parts.device
     if nparts == 1:
         return parts.slice(0, m)
     seg = torch.arange(nparts * m, device=dev) % m
-    folded, ids = _fold_segments(pk, parts, seg)
-    out = CiphertextVector.zeros(m, pk._key.L2, dev)
-    out._assign(ids, folded)
-    out.n = pk.n
-    return out
+    return _fold_to_segments(pk, parts, seg, m)
 
 
 def fold_across_ranks(pk, hist, group=None):

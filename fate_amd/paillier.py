@@ -766,17 +766,20 @@ class CiphertextVector:
     def iupdate(self, other: "CiphertextVector", indexes, stride: int, pk: "PK") -> None:
         """``CiphertextVector::iupdate`` (lib.rs:724-735): data[pos*stride+t] += other[i*stride+t]
         for every position pos listed for sample i, folded per target slot on the device."""
-        ii, pp = _flatten_positions(indexes)
+        ii, pp = _flatten_positions(indexes, self.device)
         self._scatter_fold(other, ii, pp, stride, pk)
 
     def iupdate_with_masks(self, other: "CiphertextVector", indexes, masks, stride: int, pk: "PK") -> None:
         """``CiphertextVector::iupdate_with_masks`` (lib.rs:736-747): the k-th position list
         belongs to the k-th sample whose mask is true."""
         m = torch.as_tensor(list(masks) if not isinstance(masks, torch.Tensor) else masks, dtype=torch.bool)
-        vpos = torch.nonzero(m).squeeze(1)
-        ii, pp = _flatten_positions(indexes)
+        vpos = torch.nonzero(m.to(self.device)).squeeze(1).to(torch.int32)
+        ii, pp = _flatten_positions(indexes, self.device)
         if ii.numel():
-            ii = vpos[ii]
+            if int(ii.max()) >= vpos.numel():  # more position lists than true masks: the reference's zip stops
+                keep = ii < vpos.numel()
+                ii, pp = ii[keep], pp[keep]
+            ii = vpos[ii.long()]
         self._scatter_fold(other, ii, pp, stride, pk)
 
     def _scatter_fold(self, other: "CiphertextVector", ii: torch.Tensor, pp: torch.Tensor, stride: int,
@@ -789,14 +792,15 @@ class CiphertextVector:
         if ii.numel() == 0:
             return
         dev = self.device
-        ii, pp = ii.to(dev), pp.to(dev)
+        ii, pp = ii.to(dev, torch.int64), pp.to(dev, torch.int64)
         t = torch.arange(stride, device=dev)
         src = (ii[:, None] * stride + t).reshape(-1)
         slot = (pp[:, None] * stride + t).reshape(-1)
-        if int(slot.max()) >= self.count or int(src.max()) >= other.count:
-            raise PanicException("index out of bounds")
-        folded, ids = _fold_segments(pk, other, slot, index=src)
-        self._assign(ids, _add(pk, self._gather(ids), folded, broadcast=False))
+        # one ciphertext per slot (the literal 1 where no term lands: add's identity), then
+        # data[s] = add(data[s], fold(terms of s)) for every slot at once
+        folded = _fold_to_segments(pk, other, slot, self.count, index=src)
+        r = _add(pk, _fit_limbs(self, pk._key.L2), folded, broadcast=False)
+        self.C, self.sign, self.exp = r.C, r.sign, r.exp
 
     def chunking_cumsum_with_step(self, pk: "PK", chunk_sizes: Sequence[int], step: int) -> None:
         """``CiphertextVector::chunking_cumsum_with_step`` (lib.rs:760-771): within each chunk,
@@ -824,7 +828,6 @@ class CiphertextVector:
                                 ) -> "CiphertextVector":
         """``CiphertextVector::intervals_sum_with_step`` (lib.rs:773-788): out[i*step + c] =
         fold of data[s+k] over k = c (mod step), s+k < e, from zero."""
-        out = CiphertextVector.zeros(len(intervals) * step, self.L2, self.device)
         idx, seg = [], []
         for i, (s_, e_) in enumerate(intervals):
             if e_ > self.count or s_ > e_:
@@ -832,12 +835,10 @@ class CiphertextVector:
             k = torch.arange(s_, e_)
             idx.append(k)
             seg.append(i * step + (k - s_) % step)
-        if idx:
-            ia, sa_ = torch.cat(idx), torch.cat(seg)
-            if ia.numel():
-                folded, ids = _fold_segments(pk, self, sa_, index=ia)
-                out._assign(ids, folded)
-        return out
+        nout = len(intervals) * step
+        if not idx or sum(k.numel() for k in idx) == 0:
+            return CiphertextVector.zeros(nout, self.L2, self.device)
+        return _fold_to_segments(pk, self, torch.cat(seg), nout, index=torch.cat(idx))
 
     def pack_squeeze(self, pack_num: int, offset_bit: int, pk: "PK") -> "CiphertextVector":
         """``CiphertextVector::pack_squeeze`` (paillier.rs:241; lib.rs:439-450): per chunk of
@@ -974,19 +975,24 @@ def _add(pk: "PK", a: CiphertextVector, b: CiphertextVector, broadcast: bool, co
     return out
 
 
-def _flatten_positions(indexes) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Vec<Vec<usize>> of positions per sample -> (sample ids, positions), flat."""
+def _flatten_positions(indexes, dev=None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Vec<Vec<usize>> of positions per sample -> (sample ids, positions), flat int32 on `dev`.
+    A [samples, positions] tensor is expanded on the device (no host-side index arrays)."""
     if isinstance(indexes, torch.Tensor):
         if indexes.dim() != 2:
             raise ValueError("positions tensor must be 2-D [samples, positions]")
         ns, npos = indexes.shape
-        return torch.arange(ns).repeat_interleave(npos), indexes.reshape(-1).long().cpu()
+        if (ns * npos) >= (1 << 31):
+            raise ValueError("iupdate: more than 2^31 - 1 positions in one call")
+        pp = indexes.to(device=dev, dtype=torch.int32).reshape(-1)
+        ii = torch.arange(ns * npos, device=dev, dtype=torch.int32) // max(npos, 1)
+        return ii, pp
     lens = [len(x) for x in indexes]
     if sum(lens) == 0:
-        return torch.zeros(0, dtype=torch.long), torch.zeros(0, dtype=torch.long)
+        return torch.zeros(0, dtype=torch.int32, device=dev), torch.zeros(0, dtype=torch.int32, device=dev)
     ii = torch.arange(len(lens)).repeat_interleave(torch.tensor(lens))
     pp = torch.tensor(list(itertools.chain.from_iterable(indexes)), dtype=torch.long)
-    return ii, pp
+    return ii.to(dev, torch.int32), pp.to(dev, torch.int32)
 
 
 FOLD_MAX = 64  # terms per chunk of fphe_fold (kFoldMax in kernels27.h)
@@ -1065,6 +1071,44 @@ def _fold_segments(pk: "PK", src: CiphertextVector, seg: torch.Tensor, index: Op
         li = torch.nonzero(lit).squeeze(1)
         res.exp[li] = texp[last[ids[li]]]
     return res, ids
+
+
+def _fold_to_segments(pk: "PK", src: CiphertextVector, seg: torch.Tensor, nseg: int,
+                      index: Optional[torch.Tensor] = None) -> CiphertextVector:
+    """out[s] = the reference's sequential ct-add fold of the terms src[index[t]] with seg[t] == s,
+    for every s < nseg (the literal 1, exp 0, where no term lands) -- fphe_fold_segments, which
+    groups, folds and merges the exponents on the device.  Falls back to the torch grouping of
+    :func:`_fold_segments` when the (segment, exponent) key space is too large for it."""
+    dev = src.device
+    src = _fit_limbs(src, pk._key.L2)
+    L2 = pk._key.L2
+    seg = seg.to(dev, torch.int32).contiguous()
+    T = seg.numel()
+    idx = None if index is None else index.to(dev, torch.int32).contiguous()
+    if idx is not None and idx.numel() != T:
+        raise ValueError("fold: index and segment arrays differ in length")
+    out = CiphertextVector.empty(nseg, L2, dev)
+    out.n = pk.n
+    if nseg == 0:
+        if T:
+            raise PanicException("index out of bounds")
+        return out
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    st = _lib.load().fphe_fold_segments(pk._key.ctx(dev), _ptr(src.C), _ptr(src.sign), _ptr(src.exp), src.count,
+                                        _ptr(idx), _ptr(seg), T, nseg, _ptr(out.C), _ptr(out.sign), _ptr(out.exp),
+                                        None, _ptr(err), ctypes.c_void_p(_stream(dev)))
+    if st == _lib.FPHE_ERR_RANGE:
+        res, ids = _fold_segments(pk, src, seg.long(), index=None if idx is None else idx.long())
+        out = CiphertextVector.zeros(nseg, L2, dev)
+        out._assign(ids, res)
+        out.n = pk.n
+        return out
+    if st == _lib.FPHE_ERR_ARG:
+        raise PanicException("index out of bounds")
+    _lib.check(st, "fphe_fold_segments")
+    if int(err.item()) & _lib.EF_EXP_RANGE:
+        raise ValueError(f"exponent gap beyond {MAX_GAP} in a fold: corrupt exponents")
+    return out
 
 
 def _is_literal_one(v: CiphertextVector) -> torch.Tensor:
@@ -1170,10 +1214,9 @@ def _matmul_terms(pk: "PK", a: CiphertextVector, b: PlaintextVector, ai: torch.T
     for s0 in range(0, ai.numel(), chunk):
         sl = slice(s0, s0 + chunk)
         prod = _mul(pk, a._gather(ai[sl]), b._gather(bi[sl].to(b.device)), broadcast=False)
-        folded, ids = _fold_segments(pk, prod, oi[sl])
-        if s0:  # the running partial sums come first: fold(out, terms) = add(out, fold(terms))
-            folded = _add(pk, out._gather(ids), folded, broadcast=False)
-        out._assign(ids, folded)
+        folded = _fold_to_segments(pk, prod, oi[sl], nout)
+        # the running partial sums come first: fold(out, terms) = add(out, fold(terms))
+        out = folded if s0 == 0 else _add(pk, out, folded, broadcast=False)
     return out
 
 

@@ -45,6 +45,9 @@ typedef enum {
   FPHE_ERR_HIP = 2,        /* HIP runtime error (allocation, launch) */
   FPHE_ERR_NO_SK = 3,      /* decrypt on a public-only context */
   FPHE_ERR_KEY = 4,        /* key material rejected (even modulus, p == q, ...) */
+  FPHE_ERR_RANGE = 5,      /* fphe_fold_segments: (segment, exponent) key space too large for the
+                              device grouping (nseg x exponent range > 2^25); nothing was written
+                              but the initialised outputs: the caller folds another way */
 } fphe_status;
 
 /* Per-element error bits written (OR-ed) into the caller's device `err` word. */
@@ -54,6 +57,7 @@ typedef enum {
 #define FPHE_EF_MUL_INVALID_PT     0x08u  /* "invalid plaintext" (lib.rs:342-343) */
 #define FPHE_EF_NOT_INVERTIBLE     0x10u  /* invert(...).unwrap() on a non-unit (math/src/rug/mod.rs:30-35) */
 #define FPHE_EF_DECODE_I128        0x20u  /* decode_i64: "cant't convert to i128" (lib.rs:130-142) */
+#define FPHE_EF_EXP_RANGE          0x40u  /* an exponent gap beyond 65536 in a fold (corrupt exponents) */
 
 typedef struct fphe_ctx fphe_ctx;
 
@@ -194,6 +198,24 @@ fphe_status fphe_neg(fphe_ctx* ctx, const uint32_t* C, size_t count, uint32_t* C
 fphe_status fphe_fold(fphe_ctx* ctx, const uint32_t* Src, const uint8_t* ssign, const int32_t* sexp,
                       const int64_t* ord, const int64_t* cstart, const int32_t* clen, size_t nchunks,
                       uint32_t* Co, uint8_t* so, int32_t* eo, void* stream);
+
+/* Segmented ciphertext fold with the grouping on the device: for every segment s < nseg,
+ *   out[s] = Ciphertext::add-fold of Src[idx[t]] over the terms t with seg[t] == s
+ * -- the sequential folds of CiphertextVector::iupdate / iupdate_with_masks (paillier.rs:
+ * 261-283; fixedpoint_paillier/src/lib.rs:724-747), intervals_sum_with_step (:773-788) and the
+ * matmul / rmatmul sums (:861-908), which are order independent (exponent alignment by
+ * decrese_exp_to included, lib.rs:250-258,301-333).  Src is a tile-major ciphertext vector of
+ * nsrc elements; idx (int32, may be NULL: term t reads element t) and seg (int32) have nterms
+ * entries.  Outputs are tile-major [ceil(nseg/64)] vectors: a segment without terms gets the
+ * reference's zero (the literal 1, exp 0) and present[s] = 0 (present may be NULL); a segment
+ * whose fold is the literal 1 takes the exponent of its last term, as the sequential fold.
+ * Terms are counting-sorted by (segment, exponent) on the device, each run folded by chunked
+ * Montgomery products, every segment's per-exponent partials aligned to its least exponent and
+ * folded.  FPHE_ERR_ARG for an index or segment out of range; FPHE_ERR_RANGE when nseg x the
+ * exponent range exceeds 2^25 buckets.  Synchronises the stream a few times (sizes). */
+fphe_status fphe_fold_segments(fphe_ctx* ctx, const uint32_t* Src, const uint8_t* ssign, const int32_t* sexp,
+                               size_t nsrc, const int32_t* idx, const int32_t* seg, size_t nterms, size_t nseg,
+                               uint32_t* Co, uint8_t* so, int32_t* eo, uint8_t* present, int32_t* err, void* stream);
 
 /* Co = Ca^(2^nsq) * Cb mod n^2 with so = sb: the step of CiphertextVector::pack_squeeze
  * (paillier.rs:241-243; fixedpoint_paillier/src/lib.rs:439-450), `result.pow_mod_mut(2^shift)`

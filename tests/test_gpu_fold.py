@@ -1,0 +1,135 @@
+"""The device-grouped segmented fold (fphe_fold_segments, fate_amd.paillier._fold_to_segments):
+the engine under iupdate / iupdate_with_masks / intervals_sum_with_step / matmul and the
+cross-rank histogram fold.  Bit-exact against the oracle's sequential Ciphertext::add folds
+(fixedpoint_paillier/src/lib.rs:301-333, 724-791) and against the torch grouping it replaces,
+on: wide and outlier exponents (alignment by up to tens of base-16 steps), negative signed
+ciphertexts, literal-1 terms (all-literal segments end on their last term's exponent), empty
+segments, several fold levels (runs longer than 64 x 64 terms), the fallback when the
+(segment, exponent) key space is too large, and out-of-range indexes (the reference panics)."""
+import random
+
+import pytest
+import torch
+
+from fate_amd import paillier as P
+from oracle import paillier_oracle as O
+
+from test_gpu_ops import dev_vec, host, load, more  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(params=[1024, 2048], scope="module")
+def env(request):
+    return load(request.param)
+
+
+def oracle_fold(opk, src, idx, seg, nseg):
+    out = [O.ct_zero() for _ in range(nseg)]
+    for i, s in zip(idx, seg):
+        out[s] = O.ct_add(opk, out[s], src[i])
+    return [(c.c, c.exp) for c in out]
+
+
+def mixed_sources(opk, cts, k, seed):
+    """k signed ciphertexts: random integers with exponents spread over -40..18 (the bench's
+    outliers), a sprinkling of literal 1s with their own exponents."""
+    rng = random.Random(seed)
+    src = more(opk, cts, k, seed)
+    out = []
+    for c in src:
+        r = rng.random()
+        if r < 0.06:
+            out.append(O.Ciphertext(1, rng.choice([0, -14, -3, 5])))  # the reference's zero
+        elif r < 0.10:
+            out.append(O.Ciphertext(c.c, rng.choice([-40, -38, 18, 17])))
+        else:
+            out.append(O.Ciphertext(c.c, rng.choice([-14, -13, -13, -12, -15, -16])))
+    return out
+
+
+def test_fold_segments_vs_oracle(env):
+    fx, sk, pk, coder, opk, cts = env
+    rng = random.Random(5)
+    src = mixed_sources(opk, cts, 160, 5)
+    nseg = 23
+    T = 700
+    idx = [rng.randrange(len(src)) for _ in range(T)]
+    seg = [rng.randrange(nseg - 3) for _ in range(T)]  # the last 3 segments stay empty
+    # an all-literal segment: its fold is 1 with the exponent of its last term
+    lits = [i for i, c in enumerate(src) if c.c == 1]
+    for k, i in enumerate(lits[:4]):
+        idx.append(i)
+        seg.append(nseg - 4)
+    got = P._fold_to_segments(pk, dev_vec(pk, src), torch.tensor(seg), nseg, index=torch.tensor(idx))
+    assert host(pk, got) == oracle_fold(opk, src, idx, seg, nseg)
+
+
+def test_fold_segments_many_levels_and_torch_grouping(env):
+    """Runs of ~9K terms (three fold levels) on few segments, against the torch grouping."""
+    fx, sk, pk, coder, opk, cts = env
+    src = mixed_sources(opk, cts, 300, 9)
+    v = dev_vec(pk, src)
+    g = torch.Generator().manual_seed(3)
+    T = 40000
+    idx = torch.randint(0, len(src), (T,), generator=g)
+    seg = torch.randint(0, 5, (T,), generator=g)
+    got = P._fold_to_segments(pk, v, seg, 6, index=idx)
+    res, ids = P._fold_segments(pk, v, seg, index=idx)
+    want = P.CiphertextVector.zeros(6, pk._key.L2)
+    want._assign(ids, res)
+    assert host(pk, got) == host(pk, want)
+    # and segment 0 against the oracle (a strided subset of its terms keeps this quick)
+    sel = torch.nonzero(seg == 0).squeeze(1)[::17]
+    got0 = P._fold_to_segments(pk, v, torch.zeros(sel.numel(), dtype=torch.long), 1, index=idx[sel])
+    assert host(pk, got0) == oracle_fold(opk, src, idx[sel].tolist(), [0] * sel.numel(), 1)
+
+
+def test_fold_segments_identity_index_and_fallback(env):
+    """index=None (term t is element t: the cross-rank fold), and a key space beyond the
+    device grouping's 2^25 buckets (exponents far apart in different segments) that takes the
+    torch grouping instead -- same integers."""
+    fx, sk, pk, coder, opk, cts = env
+    src = mixed_sources(opk, cts, 200, 11)
+    m = 40
+    seg = [t % m for t in range(len(src))]
+    got = P._fold_to_segments(pk, dev_vec(pk, src), torch.tensor(seg), m)
+    assert host(pk, got) == oracle_fold(opk, src, list(range(len(src))), seg, m)
+    far = [O.Ciphertext(c.c, (-30000 if i % 2 else 30000) + (i % 3)) for i, c in enumerate(src)]
+    segf = [i % 2 + 2 * (i % 700) for i in range(len(far))]  # 1400 segments x 60003 exponents
+    got = P._fold_to_segments(pk, dev_vec(pk, far), torch.tensor(segf), 1400)
+    assert host(pk, got) == oracle_fold(opk, far, list(range(len(far))), segf, 1400)
+
+
+def test_fold_segments_bad_index_panics(env):
+    fx, sk, pk, coder, opk, cts = env
+    v = dev_vec(pk, more(opk, cts, 10))
+    with pytest.raises(P.PanicException):
+        P._fold_to_segments(pk, v, torch.tensor([0, 1]), 2, index=torch.tensor([0, 10]))
+    with pytest.raises(P.PanicException):
+        P._fold_to_segments(pk, v, torch.tensor([0, 2]), 2, index=torch.tensor([0, 1]))
+    hist = P.CiphertextVector.zeros(4, pk._key.L2)
+    with pytest.raises(P.PanicException):
+        hist.iupdate(v, [[0], [4]], 1, pk)
+
+
+def test_iupdate_tensor_positions_device(env):
+    """iupdate with a [samples, positions] tensor (expanded on the device) and with masks, from
+    a non-empty histogram, against the oracle."""
+    fx, sk, pk, coder, opk, cts = env
+    rng = random.Random(8)
+    src = mixed_sources(opk, cts, 120, 8)  # 60 samples x stride 2
+    data = mixed_sources(opk, cts, 24, 81)  # 12 bins x stride 2
+    pos = torch.tensor([[rng.randrange(12) for _ in range(3)] for _ in range(60)])
+    hist = dev_vec(pk, data)
+    hist.iupdate(dev_vec(pk, src), pos, 2, pk)
+    od = list(data)
+    O.iupdate(opk, od, src, pos.tolist(), 2)
+    assert host(pk, hist) == [(c.c, c.exp) for c in od]
+    masks = [rng.random() < 0.6 for _ in range(60)]
+    k = sum(masks)
+    hist2 = dev_vec(pk, data)
+    hist2.iupdate_with_masks(dev_vec(pk, src), pos[:k].tolist(), masks, 2, pk)
+    od2 = list(data)
+    O.iupdate_with_masks(opk, od2, src, pos[:k].tolist(), masks, 2)
+    assert host(pk, hist2) == [(c.c, c.exp) for c in od2]
