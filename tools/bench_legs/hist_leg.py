@@ -29,7 +29,7 @@ if len(sys.argv) > 3 and sys.argv[3] == "mul":
 bins = torch.randint(0, NB, (N, HF), generator=g)
 positions = bins + torch.arange(HF) * NB
 T = {}
-orig = {name: getattr(P, name) for name in ("_fold_segments", "_fold_chunks", "_fold_tree", "_add", "_add_order")}
+orig = {name: getattr(P, name) for name in ("_fold_to_segments", "_fold_segments", "_fold_chunks", "_fold_tree", "_add", "_add_order")}
 
 
 def timed(name):
