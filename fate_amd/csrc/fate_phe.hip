@@ -856,25 +856,31 @@ fphe_status launch_fold_segments(fphe_ctx* c, const u32* Src, const u8* ssign, c
   const int64_t NE = (int64_t)h[1] - h[0] + 1;
   if (NE < 1 || (size_t)NE * nseg > kMaxFoldKeys) return FPHE_ERR_RANGE;
   const size_t nkeys = (size_t)NE * nseg;
+  // counter copies against atomic contention on hot keys (k_gr_keys), while they stay small
+  const int32_t R = nkeys <= ((size_t)1 << 22) ? 8 : 1;
   // 2. element-major copy of the source (the fold gathers whole rows)
   u32* rows = B.get<u32>(nsrc * L);
   int32_t* keys = B.get<int32_t>(T);
+  int32_t* cntR = B.get<int32_t>(nkeys * R);
+  int32_t* offR = B.get<int32_t>(nkeys * R);
+  int32_t* fill = B.get<int32_t>(nkeys * R);
   int32_t* cnt = B.get<int32_t>(nkeys);
   int32_t* off = B.get<int32_t>(nkeys);
-  int32_t* fill = B.get<int32_t>(nkeys);
   int32_t* last = B.get<int32_t>(nseg);
+  u8* litseg = B.get<u8>(nseg);
   int32_t* ord = B.get<int32_t>(T);
   if (!B.ok) return FPHE_ERR_HIP;
   hipLaunchKernelGGL(k_tiles_to_rows<L>, dim3((unsigned)std::min<size_t>(ntiles_of(nsrc), (size_t)c->cus * 8)),
                      dim3(kGrBlock), 0, s, Src, nsrc, rows);
   // 3. keys, counts, counting sort
-  if (hipMemsetAsync(cnt, 0, nkeys * 4, s) != hipSuccess || hipMemsetAsync(fill, 0, nkeys * 4, s) != hipSuccess ||
-      hipMemsetAsync(last, 0xff, nseg * 4, s) != hipSuccess)
+  if (hipMemsetAsync(cntR, 0, nkeys * R * 4, s) != hipSuccess || hipMemsetAsync(fill, 0, nkeys * R * 4, s) != hipSuccess ||
+      hipMemsetAsync(last, 0xff, nseg * 4, s) != hipSuccess || hipMemsetAsync(litseg, 0, nseg, s) != hipSuccess)
     return FPHE_ERR_HIP;
   hipLaunchKernelGGL(k_gr_keys, dim3(gr_grid(T, c->cus)), dim3(kGrBlock), 0, s, idx, seg, sexp, T, h[0], (int32_t)NE,
-                     keys, cnt, last);
-  if (dev_scan(c, cnt, nkeys, off, nullptr, B) != FPHE_OK) return FPHE_ERR_HIP;
-  hipLaunchKernelGGL(k_gr_scatter, dim3(gr_grid(T, c->cus)), dim3(kGrBlock), 0, s, keys, idx, T, off, fill, ord);
+                     R, keys, cntR);
+  if (dev_scan(c, cntR, nkeys * R, offR, nullptr, B) != FPHE_OK) return FPHE_ERR_HIP;
+  hipLaunchKernelGGL(k_gr_keysum, dim3(gr_grid(nkeys, c->cus)), dim3(kGrBlock), 0, s, cntR, offR, nkeys, R, cnt, off);
+  hipLaunchKernelGGL(k_gr_scatter, dim3(gr_grid(T, c->cus)), dim3(kGrBlock), 0, s, keys, idx, T, R, offR, fill, ord);
   // 4. fold every (segment, exponent) run to one partial
   FoldOut P{};
   if (fold_runs<L>(c, FoldLevel{rows, ssign, sexp, ord, cnt, off, nkeys, (int32_t)T}, T, P, B) != FPHE_OK)
@@ -918,7 +924,7 @@ fphe_status launch_fold_segments(fphe_ctx* c, const u32* Src, const u8* ssign, c
         return FPHE_ERR_HIP;
       hipLaunchKernelGGL(k_gr_gapkeys, dim3(gp), dim3(kGrBlock), 0, s, gap, P.n, gmax, gk, gc);
       if (dev_scan(c, gc, ng, go, nullptr, B) != FPHE_OK) return FPHE_ERR_HIP;
-      hipLaunchKernelGGL(k_gr_scatter, dim3(gp), dim3(kGrBlock), 0, s, gk, (const int32_t*)nullptr, P.n, go, gf, gord);
+      hipLaunchKernelGGL(k_gr_scatter, dim3(gp), dim3(kGrBlock), 0, s, gk, (const int32_t*)nullptr, P.n, 1, go, gf, gord);
       auto ka = KS<TPI>::template align_rows<L>();
       const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
       set_lds(ka, lds);
@@ -939,7 +945,10 @@ fphe_status launch_fold_segments(fphe_ctx* c, const u32* Src, const u8* ssign, c
   const int32_t nf = (int32_t)P.n;
   if (hipMemcpyAsync(nfin, &nf, 4, hipMemcpyHostToDevice, s) != hipSuccess) return FPHE_ERR_HIP;
   hipLaunchKernelGGL(k_gr_final<L>, dim3(gr_grid(P.n * 64, c->cus)), dim3(kGrBlock), 0, s, P.rows, P.sign, P.exp, P.key,
-                     nfin, last, idx, sexp, Co, so, eo, present);
+                     nfin, litseg, Co, so, eo, present);
+  // literal-1 results end on their segment's last term's exponent
+  hipLaunchKernelGGL(k_gr_last, dim3(gr_grid(T, c->cus)), dim3(kGrBlock), 0, s, seg, T, litseg, last);
+  hipLaunchKernelGGL(k_gr_litexp, dim3(gr_grid(nseg, c->cus)), dim3(kGrBlock), 0, s, nseg, litseg, last, idx, sexp, eo);
   return hip_ok(hipGetLastError());
 }
 

@@ -70,19 +70,52 @@ __global__ __launch_bounds__(kGrBlock) void k_gr_minmax(const int32_t* __restric
 }
 
 // --- pass 2: keys and counts ----------------------------------------------------------------
-// key = seg * NE + (exp - emin); cnt[key] += 1; last[seg] = max term position (the reference's
-// sequential fold ends on the segment's last term: the exponent of an all-literal-1 segment).
+// key = seg * NE + (exp - emin).  The counters are replicated R times (cnt[key * R + c], copy
+// c = (t >> 8) mod R for term t): a histogram's few hot keys take millions of atomics, and R
+// copies divide that contention; the scan over the key-major copies gives every (key, copy)
+// its own output range, so the scatter pass uses the same copy and needs no other change.
+constexpr int kCopyShift = 8;
 __global__ __launch_bounds__(kGrBlock) void k_gr_keys(const int32_t* __restrict__ idx, const int32_t* __restrict__ seg,
                                                       const int32_t* __restrict__ sexp, size_t T, int32_t emin, int32_t NE,
-                                                      int32_t* __restrict__ keys, int32_t* __restrict__ cnt,
-                                                      int32_t* __restrict__ last) {
+                                                      int32_t R, int32_t* __restrict__ keys, int32_t* __restrict__ cnt) {
   for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < T; t += (size_t)gridDim.x * blockDim.x) {
     const int32_t s = idx ? idx[t] : (int32_t)t;
-    const int32_t g = seg[t];
-    const int32_t k = g * NE + (sexp[s] - emin);
+    const int32_t k = seg[t] * NE + (sexp[s] - emin);
     keys[t] = k;
-    atomicAdd(&cnt[k], 1);
-    atomicMax(&last[g], (int32_t)t);
+    atomicAdd(&cnt[(size_t)k * R + ((t >> kCopyShift) % R)], 1);
+  }
+}
+
+// per key: the copies' total and the first copy's offset
+__global__ __launch_bounds__(kGrBlock) void k_gr_keysum(const int32_t* __restrict__ cntR, const int32_t* __restrict__ offR,
+                                                        size_t nkeys, int32_t R, int32_t* __restrict__ cnt,
+                                                        int32_t* __restrict__ off) {
+  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < nkeys; k += (size_t)gridDim.x * blockDim.x) {
+    int32_t c = 0;
+    for (int r = 0; r < R; ++r) c += cntR[k * R + r];
+    cnt[k] = c;
+    off[k] = offR[k * R];
+  }
+}
+
+// last[seg] = the position of the segment's last term, for the segments flagged in litseg
+// only (a fold that ends as the literal 1 takes its last term's exponent: the reference's
+// sequential fold ends on that term, lib.rs:303-308); other segments cost one flag read
+__global__ __launch_bounds__(kGrBlock) void k_gr_last(const int32_t* __restrict__ seg, size_t T,
+                                                      const u8* __restrict__ litseg, int32_t* __restrict__ last) {
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < T; t += (size_t)gridDim.x * blockDim.x) {
+    const int32_t g = seg[t];
+    if (litseg[g]) atomicMax(&last[g], (int32_t)t);
+  }
+}
+
+__global__ __launch_bounds__(kGrBlock) void k_gr_litexp(size_t nseg, const u8* __restrict__ litseg,
+                                                        const int32_t* __restrict__ last, const int32_t* __restrict__ idx,
+                                                        const int32_t* __restrict__ sexp, int32_t* __restrict__ eo) {
+  for (size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x; s < nseg; s += (size_t)gridDim.x * blockDim.x) {
+    if (!litseg[s]) continue;
+    const int32_t t = last[s];
+    eo[s] = sexp[idx ? idx[t] : t];
   }
 }
 
@@ -178,14 +211,14 @@ __global__ __launch_bounds__(kGrBlock) void k_scan_add(int32_t* __restrict__ out
 }
 
 // --- pass 3: counting-sort scatter ------------------------------------------------------------
-// ord[off[key] + rank] = source index of the term (rank by an atomic cursor: the order within a
-// key is arbitrary, the fold does not depend on it)
+// ord[off[key * R + c] + rank] = source index of the term (rank by an atomic cursor of the
+// term's copy c: the order within a key is arbitrary, the fold does not depend on it)
 __global__ __launch_bounds__(kGrBlock) void k_gr_scatter(const int32_t* __restrict__ keys, const int32_t* __restrict__ idx,
-                                                         size_t T, const int32_t* __restrict__ off,
+                                                         size_t T, int32_t R, const int32_t* __restrict__ off,
                                                          int32_t* __restrict__ fill, int32_t* __restrict__ ord) {
   for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < T; t += (size_t)gridDim.x * blockDim.x) {
-    const int32_t k = keys[t];
-    const int32_t pos = off[k] + atomicAdd(&fill[k], 1);
+    const size_t kc = (size_t)keys[t] * R + ((t >> kCopyShift) % R);
+    const int32_t pos = off[kc] + atomicAdd(&fill[kc], 1);
     ord[pos] = idx ? idx[t] : (int32_t)t;
   }
 }
@@ -306,10 +339,8 @@ __global__ __launch_bounds__(kGrBlock) void k_gr_init_out(size_t nseg, u32* __re
 template <int L>
 __global__ __launch_bounds__(kGrBlock) void k_gr_final(const u32* __restrict__ rows, const u8* __restrict__ sign,
                                                        const int32_t* __restrict__ exp, const int32_t* __restrict__ pkey,
-                                                       const int32_t* __restrict__ np_dev,
-                                                       const int32_t* __restrict__ last, const int32_t* __restrict__ idx,
-                                                       const int32_t* __restrict__ sexp, u32* __restrict__ Co,
-                                                       u8* __restrict__ so, int32_t* __restrict__ eo,
+                                                       const int32_t* __restrict__ np_dev, u8* __restrict__ litseg,
+                                                       u32* __restrict__ Co, u8* __restrict__ so, int32_t* __restrict__ eo,
                                                        u8* __restrict__ present) {
   const int32_t np = *np_dev;
   // one wave per partial: lanes copy words, lane 0 the per-element fields
@@ -327,12 +358,8 @@ __global__ __launch_bounds__(kGrBlock) void k_gr_final(const u32* __restrict__ r
     const bool one = __ballot(acc != 0) == 0 && sign[p] == 0;
     if (lane == 0) {
       so[s] = sign[p];
-      int32_t e = exp[p];
-      if (one) {
-        const int32_t t = last[s];
-        e = sexp[idx ? idx[t] : t];
-      }
-      eo[s] = e;
+      eo[s] = exp[p];  // a literal-1 result's exponent is set by k_gr_litexp
+      litseg[s] = one ? 1 : 0;
       if (present) present[s] = 1;
     }
   }

@@ -27,6 +27,10 @@
 #ifndef FPHE_FOLD_OCC
 #define FPHE_FOLD_OCC 2
 #endif
+// the fold's term prefetch one product ahead (35 VGPRs held across the product: 2 waves)
+#ifndef FPHE_FOLD_PF
+#define FPHE_FOLD_PF 1
+#endif
 #define FPHE_OCC_MISC __attribute__((amdgpu_waves_per_eu(FPHE_MISC_OCC)))
 #define FPHE_OCC_FOLD __attribute__((amdgpu_waves_per_eu(FPHE_FOLD_OCC)))
 #define FPHE_OCC_ENC __attribute__((amdgpu_waves_per_eu(FPHE_ENC_OCC)))

@@ -798,8 +798,15 @@ class CiphertextVector:
         slot = (pp[:, None] * stride + t).reshape(-1)
         # one ciphertext per slot (the literal 1 where no term lands: add's identity), then
         # data[s] = add(data[s], fold(terms of s)) for every slot at once
-        folded = _fold_to_segments(pk, other, slot, self.count, index=src)
-        r = _add(pk, _fit_limbs(self, pk._key.L2), folded, broadcast=False)
+        folded, present = _fold_to_segments(pk, other, slot, self.count, index=src, with_present=True)
+        cur = _fit_limbs(self, pk._key.L2)
+        r = _add(pk, cur, folded, broadcast=False)
+        # slots no term reaches keep their value as it was (exponent of a literal 1 included:
+        # the reference never touches them)
+        keep = present[: r.sign.numel()] == 0
+        r.C = torch.where(keep.view(-1, 1, WAVE), cur.C, r.C)
+        r.sign = torch.where(keep, cur.sign, r.sign)
+        r.exp = torch.where(keep, cur.exp, r.exp)
         self.C, self.sign, self.exp = r.C, r.sign, r.exp
 
     def chunking_cumsum_with_step(self, pk: "PK", chunk_sizes: Sequence[int], step: int) -> None:
@@ -1074,11 +1081,12 @@ def _fold_segments(pk: "PK", src: CiphertextVector, seg: torch.Tensor, index: Op
 
 
 def _fold_to_segments(pk: "PK", src: CiphertextVector, seg: torch.Tensor, nseg: int,
-                      index: Optional[torch.Tensor] = None) -> CiphertextVector:
+                      index: Optional[torch.Tensor] = None, with_present: bool = False):
     """out[s] = the reference's sequential ct-add fold of the terms src[index[t]] with seg[t] == s,
     for every s < nseg (the literal 1, exp 0, where no term lands) -- fphe_fold_segments, which
     groups, folds and merges the exponents on the device.  Falls back to the torch grouping of
-    :func:`_fold_segments` when the (segment, exponent) key space is too large for it."""
+    :func:`_fold_segments` when the (segment, exponent) key space is too large for it.
+    with_present: also return the per-segment uint8 flags "some term landed here"."""
     dev = src.device
     src = _fit_limbs(src, pk._key.L2)
     L2 = pk._key.L2
@@ -1089,26 +1097,28 @@ def _fold_to_segments(pk: "PK", src: CiphertextVector, seg: torch.Tensor, nseg: 
         raise ValueError("fold: index and segment arrays differ in length")
     out = CiphertextVector.empty(nseg, L2, dev)
     out.n = pk.n
+    present = torch.zeros(_ntiles(nseg) * WAVE, dtype=torch.uint8, device=dev)
     if nseg == 0:
         if T:
             raise PanicException("index out of bounds")
-        return out
+        return (out, present) if with_present else out
     err = torch.zeros(1, dtype=torch.int32, device=dev)
     st = _lib.load().fphe_fold_segments(pk._key.ctx(dev), _ptr(src.C), _ptr(src.sign), _ptr(src.exp), src.count,
                                         _ptr(idx), _ptr(seg), T, nseg, _ptr(out.C), _ptr(out.sign), _ptr(out.exp),
-                                        None, _ptr(err), ctypes.c_void_p(_stream(dev)))
+                                        _ptr(present), _ptr(err), ctypes.c_void_p(_stream(dev)))
     if st == _lib.FPHE_ERR_RANGE:
         res, ids = _fold_segments(pk, src, seg.long(), index=None if idx is None else idx.long())
         out = CiphertextVector.zeros(nseg, L2, dev)
         out._assign(ids, res)
         out.n = pk.n
-        return out
+        present[ids] = 1
+        return (out, present) if with_present else out
     if st == _lib.FPHE_ERR_ARG:
         raise PanicException("index out of bounds")
     _lib.check(st, "fphe_fold_segments")
     if int(err.item()) & _lib.EF_EXP_RANGE:
         raise ValueError(f"exponent gap beyond {MAX_GAP} in a fold: corrupt exponents")
-    return out
+    return (out, present) if with_present else out
 
 
 def _is_literal_one(v: CiphertextVector) -> torch.Tensor:

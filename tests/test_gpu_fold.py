@@ -105,12 +105,16 @@ def test_fold_segments_bad_index_panics(env):
     fx, sk, pk, coder, opk, cts = env
     v = dev_vec(pk, more(opk, cts, 10))
     with pytest.raises(P.PanicException):
-        P._fold_to_segments(pk, v, torch.tensor([0, 1]), 2, index=torch.tensor([0, 10]))
+        P._fold_to_segments(pk, v, torch.tensor([0, 1]), 2, index=torch.tensor([0, v.count]))
+    with pytest.raises(P.PanicException):
+        P._fold_to_segments(pk, v, torch.tensor([0, 1]), 2, index=torch.tensor([-1, 0]))
     with pytest.raises(P.PanicException):
         P._fold_to_segments(pk, v, torch.tensor([0, 2]), 2, index=torch.tensor([0, 1]))
     hist = P.CiphertextVector.zeros(4, pk._key.L2)
     with pytest.raises(P.PanicException):
-        hist.iupdate(v, [[0], [4]], 1, pk)
+        hist.iupdate(v, [[0], [4]], 1, pk)  # a position past the histogram
+    with pytest.raises(P.PanicException):
+        hist.iupdate(v, [[0]] * (v.count + 1), 1, pk)  # more samples than the source holds
 
 
 def test_iupdate_tensor_positions_device(env):
