@@ -711,7 +711,7 @@ fphe_status launch_fold27(fphe_ctx* c, const uint32_t* Src, const uint8_t* ssign
                           const int64_t* ord, const int64_t* cstart, const int32_t* clen, size_t nchunks,
                           uint32_t* Co, uint8_t* so, int32_t* eo, hipStream_t s) {
   constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = rad_ll(TPI) * TPI;
-  auto kern = KS<TPI>::template fold<L, int64_t, false>();
+  auto kern = KS<TPI>::template fold<L, int64_t, false, true>();
   const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
   set_lds(kern, lds);
   const unsigned grid = occ_grid(c, kern, lds, (nchunks + E - 1) / E, "fold27");
@@ -810,7 +810,8 @@ fphe_status fold_level(fphe_ctx* c, const FoldLevel& in, size_t nitems, FoldOut&
   if (!B.ok) return FPHE_ERR_HIP;
   hipLaunchKernelGGL(k_gr_chunks, dim3(gr_grid(in.nkeys, c->cus)), dim3(kGrBlock), 0, s, in.cnt, in.off, choff, in.nkeys,
                      k, cstart, clen, out.key);
-  auto kern = KS<TPI>::template fold<L, int32_t, true>();
+  auto kern = in.ord ? KS<TPI>::template fold<L, int32_t, true, true>()
+                     : KS<TPI>::template fold<L, int32_t, true, false>();
   const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
   set_lds(kern, lds);
   const unsigned grid = occ_grid(c, kern, lds, (nchk + E - 1) / E, "fold_segments");

@@ -49,7 +49,8 @@ def artefacts():
 def kernel_resources(path):
     rows, cur = [], None
     for line in open(path):
-        m = re.search(r"remark: [^ ]+:\d+:\d+:\s+(.*?)\s*\[-Rpass", line)
+        # "remark: FILE:L:C: TEXT [-Rpass...]" (the -save-temps build) or "FILE:L:C: remark: TEXT [...]"
+        m = re.search(r"remark:\s+(?:[^ ]+:\d+:\d+:\s+)?(.*?)\s*\[-Rpass", line)
         if not m:
             continue
         t = m.group(1)
