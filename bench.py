@@ -261,6 +261,39 @@ def add_kernel_leg(P, pk, a, b, N, stream, dev) -> dict:
     return blk
 
 
+def iupdate_roofline(src, positions, stride: int, nslots: int, seconds: float, key_bits: int) -> dict:
+    """rooflines.iupdate: the SecureBoost histogram's scatter ct-add
+    (CiphertextVector::iupdate, fixedpoint_paillier/src/lib.rs:724-735) in SURVEY.md §8(d)'s
+    MAC32 accounting, over the whole call (end to end: grouping, folds, exponent merge, the
+    final add into the histogram).  Credit: one mulmod over L = 128 per scatter-add (an aligned
+    Ciphertext::add), plus the exponent alignment at its least: 4 squarings per base-16 step
+    between each slot's largest and least term exponent (a Horner merge of the slot's
+    per-exponent partials; the reference's sequential adds align far more often).  Issued
+    work: one 28-bit general product per term (2 x 148^2 mads) plus the alignment squarings
+    actually run (each partial to its slot's least exponent) -- not counted here."""
+    dev = src.device
+    ns, npos = positions.shape
+    pos = positions.to(dev).reshape(-1).long()
+    ii = torch.arange(ns * npos, device=dev) // npos
+    t = torch.arange(stride, device=dev)
+    srci = (ii[:, None] * stride + t).reshape(-1)
+    slot = (pos[:, None] * stride + t).reshape(-1)
+    e = src.exp[srci].long()
+    emax = torch.full((nslots,), -(1 << 40), dtype=torch.long, device=dev).scatter_reduce(0, slot, e, "amax")
+    emin = torch.full((nslots,), 1 << 40, dtype=torch.long, device=dev).scatter_reduce(0, slot, e, "amin")
+    used = emax > -(1 << 40)
+    align_sq = int((4 * (emax - emin))[used].sum())
+    terms = int(slot.numel())
+    L = key_bits // 16
+    mac = (terms + align_sq) * mac32_per_mont(L)
+    blk = valu_roofline("fphe_fold_segments (k_gr_* grouping, k_fold27 levels, k_align_rows27) + k_add27",
+                        mac, seconds * 1e3, terms * (key_bits // 4 + 5) + nslots * 3 * (key_bits // 4 + 5),
+                        per_term_mac32=round(mac / terms, 1), terms=terms, slots=nslots,
+                        alignment_squarings=align_sq, scope="end to end (the whole iupdate call)")
+    blk["scatter_adds_per_s"] = round(terms / seconds, 1)
+    return blk
+
+
 def hist_packed_leg(P, pk, sk, coder, N, HF, NB, key_bits, rank, dev):
     """SecureBoost histogram on the reference's default gh-packed path (BASELINE config 4
     (ii); ml/ensemble/learner/decision_tree/hetero/guest.py:195-235, binary task): the guest
@@ -556,6 +589,7 @@ def main() -> None:
         hist.iupdate(gh, positions, 2, pk)
         torch.cuda.synchronize(dev)
         hist_s = time.perf_counter() - t0h
+        iupdate_block = iupdate_roofline(gh, positions, 2, HF * NB * 2, hist_s, key_bits)
         # property check: decrypted bins == float64 sums of the encoded inputs
         hd = coder.decode_f64_vec(sk.decrypt_to_encoded(hist)).cpu().reshape(HF * NB, 2)
         xg = x.double()
@@ -639,6 +673,7 @@ def main() -> None:
             "encrypt_keyholder_crt_equals_public_4096": crt_same,
             "ct_mul_per_s": round(N / (mul_ms / 1e3), 1),
             "histogram_scatter_adds_per_s": round(N * HF * 2 / hist_s, 1),
+            "histogram_iupdate_s": round(hist_s, 5),
             "histogram_config": f"{N} samples x {HF} features x {NB} bins x (g,h), iupdate fold on device",
             "histogram_allclose": hist_ok,
             "histogram_packed": packed,
@@ -655,6 +690,7 @@ def main() -> None:
                                          N * dec_mac32_per_elem(key_bits), dec_ms,
                                          N * (key_bits // 4 + 4 + key_bits // 8),
                                          traffic=_traffic("decrypt", N), traffic_source=pmc_ops_traffic("decrypt")[1]),
+                "iupdate": iupdate_block,
                 "ct_add": dict(add_kernel, traffic=_traffic("ct_add", N),
                                traffic_source=pmc_ops_traffic("ct_add")[1]),
                 # §8(d): float significands (E = 56): (56 + 12 + 16) mulmods over L = 128, + 3

@@ -761,9 +761,11 @@ int32_t fold_klen(size_t n) {  // chunk length: fill ~32K wave slots, 8..64 term
   return (int32_t)(k < 8 ? 8 : (k > (size_t)kFoldMax ? (size_t)kFoldMax : k));
 }
 
-// A fold level's input: n items (element-major rows + sign + exp), grouped by key in
+// A fold level's input: items (element-major rows + sign + exp), grouped by key in
 // contiguous runs: key k's items at [off[k], off[k] + cnt[k]) of the item order (ord, or the
-// items themselves when ord is null).
+// items themselves when ord is null).  Sizes past the first level live on the device (n_dev);
+// the host keeps upper bounds (n_ub items, maxcnt per key, nnz non-empty keys), so the levels
+// run back to back without reading anything back.
 struct FoldLevel {
   const u32* rows;
   const u8* sign;
@@ -772,24 +774,28 @@ struct FoldLevel {
   const int32_t* cnt;
   const int32_t* off;
   size_t nkeys;
-  int32_t maxcnt;  // largest run
+  size_t n_ub;     // items (exact on the first level)
+  int32_t maxcnt;  // largest run (bound)
+  size_t nnz;      // non-empty keys (bound)
 };
 struct FoldOut {
   u32* rows;
   u8* sign;
   int32_t* exp;
-  int32_t* key;  // key of each output partial (ascending)
-  int32_t* cnt;  // per key: partials produced
-  int32_t* off;  // per key: first partial
-  size_t n;      // partials
+  int32_t* key;    // key of each output partial (ascending)
+  int32_t* cnt;    // per key: partials produced
+  int32_t* off;    // per key: first partial
+  int32_t* n_dev;  // partials (device)
+  size_t n_ub;     // partials (bound)
   int32_t maxcnt;
 };
 
+// stats (may be null): the first level reads back {largest run, non-empty keys}
 template <int L>
-fphe_status fold_level(fphe_ctx* c, const FoldLevel& in, size_t nitems, FoldOut& out, CallBufs& B) {
+fphe_status fold_level(fphe_ctx* c, FoldLevel& in, FoldOut& out, CallBufs& B, bool read_stats) {
   constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = rad_ll(TPI) * TPI;
   hipStream_t s = B.s;
-  const int32_t k = fold_klen(nitems);
+  const int32_t k = fold_klen(in.n_ub);
   int32_t* nch = B.get<int32_t>(in.nkeys);
   int32_t* choff = B.get<int32_t>(in.nkeys);
   int32_t* hdr = B.get<int32_t>(4);
@@ -797,16 +803,21 @@ fphe_status fold_level(fphe_ctx* c, const FoldLevel& in, size_t nitems, FoldOut&
   if (hipMemsetAsync(hdr, 0, 4 * sizeof(int32_t), s) != hipSuccess) return FPHE_ERR_HIP;
   hipLaunchKernelGGL(k_gr_nchunks, dim3(gr_grid(in.nkeys, c->cus)), dim3(kGrBlock), 0, s, in.cnt, in.nkeys, k, nch, hdr);
   if (dev_scan(c, nch, in.nkeys, choff, hdr + 2, B) != FPHE_OK) return FPHE_ERR_HIP;
-  int32_t h[4];
-  if (hipMemcpyAsync(h, hdr, sizeof(h), hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
-    return FPHE_ERR_HIP;
-  const size_t nchk = (size_t)h[2];
-  int32_t* cstart = B.get<int32_t>(nchk);
-  int32_t* clen = B.get<int32_t>(nchk);
-  out.key = B.get<int32_t>(nchk);
-  out.rows = B.get<u32>(nchk * L);
-  out.sign = B.get<u8>(nchk);
-  out.exp = B.get<int32_t>(nchk);
+  if (read_stats) {
+    int32_t h[4];
+    if (hipMemcpyAsync(h, hdr, sizeof(h), hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+      return FPHE_ERR_HIP;
+    in.maxcnt = h[0];
+    in.nnz = (size_t)h[1];
+  }
+  // chunks <= sum over non-empty keys of (cnt / k + 1)
+  const size_t ub = in.n_ub / (size_t)k + in.nnz + 1;
+  int32_t* cstart = B.get<int32_t>(ub);
+  int32_t* clen = B.get<int32_t>(ub);
+  out.key = B.get<int32_t>(ub);
+  out.rows = B.get<u32>(ub * L);
+  out.sign = B.get<u8>(ub);
+  out.exp = B.get<int32_t>(ub);
   if (!B.ok) return FPHE_ERR_HIP;
   hipLaunchKernelGGL(k_gr_chunks, dim3(gr_grid(in.nkeys, c->cus)), dim3(kGrBlock), 0, s, in.cnt, in.off, choff, in.nkeys,
                      k, cstart, clen, out.key);
@@ -814,24 +825,25 @@ fphe_status fold_level(fphe_ctx* c, const FoldLevel& in, size_t nitems, FoldOut&
                      : KS<TPI>::template fold<L, int32_t, true, false>();
   const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
   set_lds(kern, lds);
-  const unsigned grid = occ_grid(c, kern, lds, (nchk + E - 1) / E, "fold_segments");
+  const unsigned grid = occ_grid(c, kern, lds, (ub + E - 1) / E, "fold_segments");
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, in.rows, in.sign, in.exp, in.ord, cstart, clen,
-                     nchk, (const int32_t*)nullptr, c->K.FR_27, out.rows, out.sign, out.exp, (u32)NL);
+                     ub, (const int32_t*)(hdr + 2), c->K.FR_27, out.rows, out.sign, out.exp, (u32)NL);
   out.cnt = nch;
   out.off = choff;
-  out.n = nchk;
+  out.n_dev = hdr + 2;
+  out.n_ub = ub;
   out.maxcnt = (in.maxcnt + k - 1) / k;
   return hip_ok(hipGetLastError());
 }
 
 // fold every key's run down to one partial (levels of chunked products)
 template <int L>
-fphe_status fold_runs(fphe_ctx* c, FoldLevel lv, size_t nitems, FoldOut& out, CallBufs& B) {
+fphe_status fold_runs(fphe_ctx* c, FoldLevel lv, FoldOut& out, CallBufs& B, bool read_stats) {
   for (;;) {
-    if (fold_level<L>(c, lv, nitems, out, B) != FPHE_OK) return FPHE_ERR_HIP;
+    if (fold_level<L>(c, lv, out, B, read_stats) != FPHE_OK) return FPHE_ERR_HIP;
+    read_stats = false;
     if (out.maxcnt <= 1) return FPHE_OK;
-    lv = FoldLevel{out.rows, out.sign, out.exp, nullptr, out.cnt, out.off, lv.nkeys, out.maxcnt};
-    nitems = out.n;
+    lv = FoldLevel{out.rows, out.sign, out.exp, nullptr, out.cnt, out.off, lv.nkeys, out.n_ub, out.maxcnt, lv.nnz};
   }
 }
 
@@ -884,69 +896,61 @@ fphe_status launch_fold_segments(fphe_ctx* c, const u32* Src, const u8* ssign, c
   hipLaunchKernelGGL(k_gr_scatter, dim3(gr_grid(T, c->cus)), dim3(kGrBlock), 0, s, keys, idx, T, R, offR, fill, ord);
   // 4. fold every (segment, exponent) run to one partial
   FoldOut P{};
-  if (fold_runs<L>(c, FoldLevel{rows, ssign, sexp, ord, cnt, off, nkeys, (int32_t)T}, T, P, B) != FPHE_OK)
-    return FPHE_ERR_HIP;
+  FoldLevel lv1{rows, ssign, sexp, ord, cnt, off, nkeys, T, (int32_t)T, std::min(nkeys, T)};
+  if (fold_runs<L>(c, lv1, P, B, true) != FPHE_OK) return FPHE_ERR_HIP;
+  const size_t nnz = std::min(nkeys, T);  // bound of the non-empty (segment, exponent) keys
   // 5. merge each segment's per-exponent partials: align to the segment's least exponent, fold
   if (NE > 1) {
+    const size_t np = P.n_ub;  // partials (bound); the exact count is P.n_dev
     int32_t* segmin = B.get<int32_t>(nseg);
-    u8* lit = B.get<u8>(P.n);
-    int32_t* gap = B.get<int32_t>(P.n);
-    int32_t* skey = B.get<int32_t>(P.n);
+    u8* lit = B.get<u8>(np);
+    int32_t* gap = B.get<int32_t>(np);
+    int32_t* skey = B.get<int32_t>(np);
     int32_t* scnt = B.get<int32_t>(nseg);
     int32_t* soff = B.get<int32_t>(nseg);
     int32_t* gh = B.get<int32_t>(2);
-    int32_t* np_dev = B.get<int32_t>(1);
     if (!B.ok) return FPHE_ERR_HIP;
-    const int32_t npi = (int32_t)P.n;
     if (hipMemsetD32Async((hipDeviceptr_t)segmin, kI32Max, nseg, s) != hipSuccess ||
-        hipMemsetAsync(scnt, 0, nseg * 4, s) != hipSuccess || hipMemsetAsync(gh, 0, 8, s) != hipSuccess ||
-        hipMemcpyAsync(np_dev, &npi, 4, hipMemcpyHostToDevice, s) != hipSuccess)
+        hipMemsetAsync(scnt, 0, nseg * 4, s) != hipSuccess || hipMemsetAsync(gh, 0, 8, s) != hipSuccess)
       return FPHE_ERR_HIP;
-    const unsigned gp = gr_grid(P.n, c->cus);
-    hipLaunchKernelGGL(k_gr_segmin<L>, dim3(gp), dim3(kGrBlock), 0, s, P.rows, P.sign, P.exp, P.key, np_dev,
+    const unsigned gp = gr_grid(np, c->cus);
+    hipLaunchKernelGGL(k_gr_segmin<L>, dim3(gp), dim3(kGrBlock), 0, s, P.rows, P.sign, P.exp, P.key, P.n_dev,
                        (int32_t)NE, segmin, lit);
-    hipLaunchKernelGGL(k_gr_gaps, dim3(gp), dim3(kGrBlock), 0, s, P.exp, P.key, lit, np_dev, (int32_t)NE, segmin, gap,
+    hipLaunchKernelGGL(k_gr_gaps, dim3(gp), dim3(kGrBlock), 0, s, P.exp, P.key, lit, P.n_dev, (int32_t)NE, segmin, gap,
                        skey, scnt, gh, err);
-    if (hipMemcpyAsync(h, gh, 8, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+    // partials in descending-gap order (counting sort on NE - 1 - gap: every gap < NE), then
+    // the alignment; waves whose partials all have gap 0 skip their tile at once
+    const size_t ng = (size_t)NE;
+    int32_t* gk = B.get<int32_t>(np);
+    int32_t* gc = B.get<int32_t>(ng);
+    int32_t* go = B.get<int32_t>(ng);
+    int32_t* gf = B.get<int32_t>(ng);
+    int32_t* gord = B.get<int32_t>(np);
+    u32* tile_ctr = B.get<u32>(1);
+    if (!B.ok) return FPHE_ERR_HIP;
+    if (hipMemsetAsync(gc, 0, ng * 4, s) != hipSuccess || hipMemsetAsync(gf, 0, ng * 4, s) != hipSuccess ||
+        hipMemsetAsync(tile_ctr, 0, 4, s) != hipSuccess)
       return FPHE_ERR_HIP;
-    const int32_t gmax = h[0];
-    if (gmax > 0) {
-      // partials in descending-gap order (counting sort on gmax - gap), then the alignment
-      const size_t ng = (size_t)gmax + 1;
-      int32_t* gk = B.get<int32_t>(P.n);
-      int32_t* gc = B.get<int32_t>(ng);
-      int32_t* go = B.get<int32_t>(ng);
-      int32_t* gf = B.get<int32_t>(ng);
-      int32_t* gord = B.get<int32_t>(P.n);
-      u32* tile_ctr = B.get<u32>(1);
-      if (!B.ok) return FPHE_ERR_HIP;
-      if (hipMemsetAsync(gc, 0, ng * 4, s) != hipSuccess || hipMemsetAsync(gf, 0, ng * 4, s) != hipSuccess ||
-          hipMemsetAsync(tile_ctr, 0, 4, s) != hipSuccess)
-        return FPHE_ERR_HIP;
-      hipLaunchKernelGGL(k_gr_gapkeys, dim3(gp), dim3(kGrBlock), 0, s, gap, P.n, gmax, gk, gc);
-      if (dev_scan(c, gc, ng, go, nullptr, B) != FPHE_OK) return FPHE_ERR_HIP;
-      hipLaunchKernelGGL(k_gr_scatter, dim3(gp), dim3(kGrBlock), 0, s, gk, (const int32_t*)nullptr, P.n, 1, go, gf, gord);
-      auto ka = KS<TPI>::template align_rows<L>();
-      const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
-      set_lds(ka, lds);
-      const unsigned ga = occ_grid(c, ka, lds, (P.n + E - 1) / E, "align_rows");
-      hipLaunchKernelGGL(ka, dim3(ga), dim3(kBlock), lds, s, c->K, P.rows, P.sign, gap, gord, np_dev, tile_ctr,
-                         (u32)NL);
-    }
+    hipLaunchKernelGGL(k_gr_gapkeys, dim3(gp), dim3(kGrBlock), 0, s, gap, P.n_dev, (int32_t)(NE - 1), gk, gc);
+    if (dev_scan(c, gc, ng, go, nullptr, B) != FPHE_OK) return FPHE_ERR_HIP;
+    hipLaunchKernelGGL(k_gr_scatter_n, dim3(gp), dim3(kGrBlock), 0, s, gk, P.n_dev, go, gf, gord);
+    auto ka = KS<TPI>::template align_rows<L>();
+    const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
+    set_lds(ka, lds);
+    const unsigned ga = occ_grid(c, ka, lds, (np + E - 1) / E, "align_rows");
+    hipLaunchKernelGGL(ka, dim3(ga), dim3(kBlock), lds, s, c->K, P.rows, P.sign, gap, gord, P.n_dev, tile_ctr,
+                       (u32)NL);
     // the partials are in (segment, exponent) order: contiguous per segment
     if (dev_scan(c, scnt, nseg, soff, nullptr, B) != FPHE_OK) return FPHE_ERR_HIP;
     FoldOut Q{};
-    if (fold_runs<L>(c, FoldLevel{P.rows, P.sign, P.exp, nullptr, scnt, soff, nseg, (int32_t)NE}, P.n, Q, B) != FPHE_OK)
-      return FPHE_ERR_HIP;
+    FoldLevel lv2{P.rows, P.sign, P.exp, nullptr, scnt, soff, nseg, np, (int32_t)std::min<int64_t>(NE, (int64_t)np),
+                  std::min(nseg, nnz)};
+    if (fold_runs<L>(c, lv2, Q, B, false) != FPHE_OK) return FPHE_ERR_HIP;
     P = Q;
   }
   // 6. scatter to the output segments (keys are segment ids here)
-  int32_t* nfin = B.get<int32_t>(1);
-  if (!B.ok) return FPHE_ERR_HIP;
-  const int32_t nf = (int32_t)P.n;
-  if (hipMemcpyAsync(nfin, &nf, 4, hipMemcpyHostToDevice, s) != hipSuccess) return FPHE_ERR_HIP;
-  hipLaunchKernelGGL(k_gr_final<L>, dim3(gr_grid(P.n * 64, c->cus)), dim3(kGrBlock), 0, s, P.rows, P.sign, P.exp, P.key,
-                     nfin, litseg, Co, so, eo, present);
+  hipLaunchKernelGGL(k_gr_final<L>, dim3(gr_grid(P.n_ub * 64, c->cus)), dim3(kGrBlock), 0, s, P.rows, P.sign, P.exp,
+                     P.key, P.n_dev, litseg, Co, so, eo, present);
   // literal-1 results end on their segment's last term's exponent
   hipLaunchKernelGGL(k_gr_last, dim3(gr_grid(T, c->cus)), dim3(kGrBlock), 0, s, seg, T, litseg, last);
   hipLaunchKernelGGL(k_gr_litexp, dim3(gr_grid(nseg, c->cus)), dim3(kGrBlock), 0, s, nseg, litseg, last, idx, sexp, eo);
@@ -1469,6 +1473,16 @@ fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, 
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) { delete c; return FPHE_ERR_HIP; }
     c->cus = prop.multiProcessorCount;
+    {
+      // fphe_fold_segments takes its scratch from the device's default stream-ordered pool:
+      // keep up to 8 GiB of it cached across calls (the default threshold of 0 hands every
+      // block back to the driver at each synchronisation, and a 1-GiB re-map costs ms)
+      hipMemPool_t pool;
+      if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+        uint64_t keep = (uint64_t)8 << 30;
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+      }
+    }
     if (hipMalloc(&c->blob, blob.size() * 4) != hipSuccess) { delete c; return FPHE_ERR_HIP; }
     if (hipMemcpy(c->blob, blob.data(), blob.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
       (void)hipFree(c->blob); delete c; return FPHE_ERR_HIP;

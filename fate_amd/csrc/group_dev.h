@@ -223,6 +223,17 @@ __global__ __launch_bounds__(kGrBlock) void k_gr_scatter(const int32_t* __restri
   }
 }
 
+// the same scatter for n items counted on the device, one copy, ord = item positions
+__global__ __launch_bounds__(kGrBlock) void k_gr_scatter_n(const int32_t* __restrict__ keys, const int32_t* __restrict__ n_dev,
+                                                           const int32_t* __restrict__ off, int32_t* __restrict__ fill,
+                                                           int32_t* __restrict__ ord) {
+  const size_t n = (size_t)*n_dev;
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (size_t)gridDim.x * blockDim.x) {
+    const int32_t k = keys[t];
+    ord[off[k] + atomicAdd(&fill[k], 1)] = (int32_t)t;
+  }
+}
+
 // --- chunk tables: key k's items [off[k], off[k] + cnt[k]) in chunks of klen ----------------------
 __global__ __launch_bounds__(kGrBlock) void k_gr_chunks(const int32_t* __restrict__ cnt, const int32_t* __restrict__ off,
                                                         const int32_t* __restrict__ choff, size_t nkeys, int32_t klen,
@@ -290,9 +301,12 @@ __global__ __launch_bounds__(kGrBlock) void k_gr_gaps(int32_t* __restrict__ exp,
   set_err(err, ef);
 }
 
-// counting-sort keys for the descending-gap order of the alignment: key = gmax - gap
-__global__ __launch_bounds__(kGrBlock) void k_gr_gapkeys(const int32_t* __restrict__ gap, size_t n, int32_t gmax,
-                                                         int32_t* __restrict__ keys, int32_t* __restrict__ cnt) {
+// counting-sort keys for the descending-gap order of the alignment: key = gmax - gap (n on
+// the device)
+__global__ __launch_bounds__(kGrBlock) void k_gr_gapkeys(const int32_t* __restrict__ gap, const int32_t* __restrict__ n_dev,
+                                                         int32_t gmax, int32_t* __restrict__ keys,
+                                                         int32_t* __restrict__ cnt) {
+  const size_t n = (size_t)*n_dev;
   for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x) {
     const int32_t k = gmax - gap[p];
     keys[p] = k;
