@@ -99,3 +99,27 @@ def tdiv_r(a: int, m: int) -> int:
     out = ctypes.create_string_buffer(cap)
     load().gref_tdiv_r(_h(a), _h(m), out, cap)
     return _int(out)
+
+
+def _batch(args):
+    """Pool worker (spawn-safe: imports nothing but this module): encrypt or decrypt a batch."""
+    op, n, p, q, items = args
+    key = GmpKey(n, p, q)
+    if op == "encrypt":
+        return [key.encrypt(m, r, r is not None) for m, r in items]
+    return [key.decrypt(c) for c in items]
+
+
+def parallel(op: str, n: int, p: int, q: int, items, procs: int = 16):
+    """op over items in `procs` spawned worker processes (fresh interpreters: safe beside a
+    GPU-initialised parent), order preserved.  op "encrypt": items are (m, r or None);
+    "decrypt": items are signed ciphertexts."""
+    import multiprocessing as mp
+    items = list(items)
+    if not items:
+        return []
+    k = max(1, -(-len(items) // procs))
+    chunks = [items[i:i + k] for i in range(0, len(items), k)]
+    with mp.get_context("spawn").Pool(min(procs, len(chunks))) as pool:
+        parts = pool.map(_batch, [(op, n, p, q, c) for c in chunks])
+    return [x for part in parts for x in part]

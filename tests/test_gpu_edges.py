@@ -186,15 +186,18 @@ def test_two_streams_share_a_context(k1024):
         assert torch.equal(y.cpu().view(torch.int32), x.cpu().view(torch.int32))
 
 
-@pytest.mark.parametrize("seed", range(3))
-def test_random_op_chains_vs_oracle(k1024, seed):
+@pytest.mark.parametrize("bits,seed", [(1024, 0), (1024, 1), (1024, 2), (2048, 0), (2048, 1)])
+def test_random_op_chains_vs_oracle(bits, seed):
     """Randomised chains of the element-wise ops (add / sub / rsub / add_pt / ct x pt with
     float, negative-float and encoded-negative-integer plaintexts / neg / i_double) over
     vectors of random ragged length, every intermediate compared bit-exact with the oracle
-    (fixedpoint_paillier/src/lib.rs:250-349)."""
+    (fixedpoint_paillier/src/lib.rs:250-349), at 1024 and 2048 bits (the starting encryptions
+    by libgmp, oracle/gmp_ref.c, which the oracle's own encrypt is pinned to)."""
     import random as _r
-    p, q, sk, pk, coder, osk, opk = k1024
-    rng = _r.Random(1000 + seed)
+    from oracle import gmp_ref
+    p, q, sk, pk, coder, osk, opk = load(bits)
+    gk = gmp_ref.GmpKey(p * q, p, q)
+    rng = _r.Random(1000 + seed + bits)
     n = rng.randrange(1, 200)
 
     def rand_pt():
@@ -210,8 +213,11 @@ def test_random_op_chains_vs_oracle(k1024, seed):
     def dev_pts(pts):
         return P.PlaintextVector.from_ints([x.significant for x in pts], [x.exp for x in pts])
 
-    oa = [O.fp_encrypt(opk, rand_pt(), True, 1 + rng.randrange(opk.n - 1)) for _ in range(n)]
-    ob = [O.fp_encrypt(opk, rand_pt(), True, 1 + rng.randrange(opk.n - 1)) for _ in range(n)]
+    def enc(pt):
+        return O.Ciphertext(gk.encrypt(pt.significant, 1 + rng.randrange(opk.n - 1), True), pt.exp)
+
+    oa = [enc(rand_pt()) for _ in range(n)]
+    ob = [enc(rand_pt()) for _ in range(n)]
     da = P.CiphertextVector.from_signed_ints([c.c for c in oa], [c.exp for c in oa], pk.ns, pk._key.L2)
     db = P.CiphertextVector.from_signed_ints([c.c for c in ob], [c.exp for c in ob], pk.ns, pk._key.L2)
     for _ in range(6):
@@ -450,3 +456,34 @@ def test_mul_spans_match_one_launch(monkeypatch):
         assert torch.equal(a.sign[:n], b.sign[:n]) and torch.equal(a.exp[:n], b.exp[:n])
     d = coder.decode_f64_vec(sk.decrypt_to_encoded(sp)).cpu()
     assert torch.allclose(d, (x.double() * w.double()).cpu(), rtol=1e-6, atol=1e-6)
+
+
+def test_config2_subset_4096_vs_gmp():
+    """SURVEY.md §8(d) config 2's bit-exact subset at full size: the first 4,096 elements of the
+    bench's 1M float32 tensor (randn * 4, seed 20241218, the edge values up front) at 2048
+    bits, with injected obfuscation nonces: the public-key encrypt, the key-holder (CRT)
+    encrypt and the CRT decrypt against libgmp (oracle/gmp_ref.c: the mpz_* sequence rug issues
+    for paillier/src/lib.rs:94-176, in 16 worker processes), and the decoded float32 bits
+    against the inputs (-0.0 decodes as +0.0, as the reference's zero significand does)."""
+    from oracle import gmp_ref
+    p, q, sk, pk, coder, osk, opk = load(2048)
+    g = torch.Generator().manual_seed(20241218)
+    x = torch.randn(1 << 20, generator=g, dtype=torch.float32) * 4
+    x[:8] = torch.tensor([0.0, -0.0, 1e-30, -1e-30, 3.4e38, -3.4e38, 1.0, -1.0])
+    x = x[:4096].contiguous()
+    pv = coder.encode_f32_vec(x.cuda())
+    sig, exp = pv.to_ints()
+    assert [(e.significant, e.exp) for e in (O.encode_f32(opk.n, v) for v in x.tolist())] == list(zip(sig, exp))
+    rng = np.random.default_rng(4096)
+    r = [1 + int.from_bytes(rng.bytes(256), "little") % (pk.n - 1) for _ in range(4096)]
+    want = gmp_ref.parallel("encrypt", p * q, p, q, list(zip(sig, r)))
+    got, got_e = P.PK(pk.n).encrypt_encoded(pv, True, r=r).to_signed_ints(pk.ns)
+    assert got_e == exp and got == want
+    ck = pk.encrypt_encoded(pv, True, r=r)  # the key holder's CRT path: the same integers
+    assert ck.to_signed_ints(pk.ns)[0] == want
+    dsig, dexp = sk.decrypt_to_encoded(ck).to_ints()
+    assert dexp == exp and dsig == gmp_ref.parallel("decrypt", p * q, p, q, want)
+    bits = coder.decode_f32_vec(sk.decrypt_to_encoded(ck)).cpu().view(torch.int32)
+    xb = x.view(torch.int32).clone()
+    xb[xb == -2147483648] = 0  # -0.0
+    assert torch.equal(bits, xb)
