@@ -716,7 +716,7 @@ fphe_status launch_fold27(fphe_ctx* c, const uint32_t* Src, const uint8_t* ssign
   set_lds(kern, lds);
   const unsigned grid = occ_grid(c, kern, lds, (nchunks + E - 1) / E, "fold27");
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, Src, ssign, sexp, ord, cstart, clen, nchunks,
-                     (const int32_t*)nullptr, c->K.FR_27, Co, so, eo, (u32)NL);
+                     (const int32_t*)nullptr, (const int32_t*)nullptr, (u32*)nullptr, c->K.FR_27, Co, so, eo, (u32)NL);
   return hip_ok(hipGetLastError());
 }
 
@@ -821,13 +821,33 @@ fphe_status fold_level(fphe_ctx* c, FoldLevel& in, FoldOut& out, CallBufs& B, bo
   if (!B.ok) return FPHE_ERR_HIP;
   hipLaunchKernelGGL(k_gr_chunks, dim3(gr_grid(in.nkeys, c->cus)), dim3(kGrBlock), 0, s, in.cnt, in.off, choff, in.nkeys,
                      k, cstart, clen, out.key);
+  // big levels: chunks handed to the waves longest first (a counting sort on the length) and
+  // wave tiles from a device counter; the outputs stay in key order (row = chunk index)
+  int32_t* cperm = nullptr;
+  u32* ctr = nullptr;
+  if (ub >= ((size_t)1 << 15)) {
+    int32_t* lk = B.get<int32_t>(ub);
+    int32_t* lc = B.get<int32_t>((size_t)k + 1);
+    int32_t* lo = B.get<int32_t>((size_t)k + 1);
+    int32_t* lf = B.get<int32_t>((size_t)k + 1);
+    cperm = B.get<int32_t>(ub);
+    ctr = B.get<u32>(1);
+    if (!B.ok) return FPHE_ERR_HIP;
+    if (hipMemsetAsync(lc, 0, (k + 1) * 4, s) != hipSuccess || hipMemsetAsync(lf, 0, (k + 1) * 4, s) != hipSuccess ||
+        hipMemsetAsync(ctr, 0, 4, s) != hipSuccess)
+      return FPHE_ERR_HIP;
+    hipLaunchKernelGGL(k_gr_lenkeys, dim3(gr_grid(ub, c->cus)), dim3(kGrBlock), 0, s, clen, hdr + 2, k, lk, lc);
+    if (dev_scan(c, lc, (size_t)k + 1, lo, nullptr, B) != FPHE_OK) return FPHE_ERR_HIP;
+    hipLaunchKernelGGL(k_gr_scatter_n, dim3(gr_grid(ub, c->cus)), dim3(kGrBlock), 0, s, lk, hdr + 2, lo, lf, cperm);
+  }
   auto kern = in.ord ? KS<TPI>::template fold<L, int32_t, true, true>()
                      : KS<TPI>::template fold<L, int32_t, true, false>();
   const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
   set_lds(kern, lds);
   const unsigned grid = occ_grid(c, kern, lds, (ub + E - 1) / E, "fold_segments");
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, in.rows, in.sign, in.exp, in.ord, cstart, clen,
-                     ub, (const int32_t*)(hdr + 2), c->K.FR_27, out.rows, out.sign, out.exp, (u32)NL);
+                     ub, (const int32_t*)(hdr + 2), (const int32_t*)cperm, ctr, c->K.FR_27, out.rows, out.sign, out.exp,
+                     (u32)NL);
   out.cnt = nch;
   out.off = choff;
   out.n_dev = hdr + 2;

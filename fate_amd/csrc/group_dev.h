@@ -234,6 +234,18 @@ __global__ __launch_bounds__(kGrBlock) void k_gr_scatter_n(const int32_t* __rest
   }
 }
 
+// counting-sort keys of the chunks by length, longest first: key = klen - len (n on device)
+__global__ __launch_bounds__(kGrBlock) void k_gr_lenkeys(const int32_t* __restrict__ clen, const int32_t* __restrict__ n_dev,
+                                                         int32_t klen, int32_t* __restrict__ keys,
+                                                         int32_t* __restrict__ cnt) {
+  const size_t n = (size_t)*n_dev;
+  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x) {
+    const int32_t k = klen - clen[p];
+    keys[p] = k;
+    atomicAdd(&cnt[k], 1);
+  }
+}
+
 // --- chunk tables: key k's items [off[k], off[k] + cnt[k]) in chunks of klen ----------------------
 __global__ __launch_bounds__(kGrBlock) void k_gr_chunks(const int32_t* __restrict__ cnt, const int32_t* __restrict__ off,
                                                         const int32_t* __restrict__ choff, size_t nkeys, int32_t klen,
