@@ -826,19 +826,24 @@ fphe_status fold_level(fphe_ctx* c, FoldLevel& in, FoldOut& out, CallBufs& B, bo
   int32_t* cperm = nullptr;
   u32* ctr = nullptr;
   if (ub >= ((size_t)1 << 15)) {
-    int32_t* lk = B.get<int32_t>(ub);
-    int32_t* lc = B.get<int32_t>((size_t)k + 1);
-    int32_t* lo = B.get<int32_t>((size_t)k + 1);
-    int32_t* lf = B.get<int32_t>((size_t)k + 1);
+    int32_t* nfull = B.get<int32_t>(in.nkeys);
+    int32_t* fulloff = B.get<int32_t>(in.nkeys);
+    int32_t* bc = B.get<int32_t>((size_t)k + 1);
+    int32_t* boff = B.get<int32_t>((size_t)k + 1);
+    int32_t* bfill = B.get<int32_t>((size_t)k + 1);
+    int32_t* nf = B.get<int32_t>(1);
     cperm = B.get<int32_t>(ub);
     ctr = B.get<u32>(1);
     if (!B.ok) return FPHE_ERR_HIP;
-    if (hipMemsetAsync(lc, 0, (k + 1) * 4, s) != hipSuccess || hipMemsetAsync(lf, 0, (k + 1) * 4, s) != hipSuccess ||
+    if (hipMemsetAsync(bc, 0, (k + 1) * 4, s) != hipSuccess || hipMemsetAsync(bfill, 0, (k + 1) * 4, s) != hipSuccess ||
         hipMemsetAsync(ctr, 0, 4, s) != hipSuccess)
       return FPHE_ERR_HIP;
-    hipLaunchKernelGGL(k_gr_lenkeys, dim3(gr_grid(ub, c->cus)), dim3(kGrBlock), 0, s, clen, hdr + 2, k, lk, lc);
-    if (dev_scan(c, lc, (size_t)k + 1, lo, nullptr, B) != FPHE_OK) return FPHE_ERR_HIP;
-    hipLaunchKernelGGL(k_gr_scatter_n, dim3(gr_grid(ub, c->cus)), dim3(kGrBlock), 0, s, lk, hdr + 2, lo, lf, cperm);
+    const unsigned gk = gr_grid(in.nkeys, c->cus);
+    hipLaunchKernelGGL(k_gr_permcnt, dim3(gk), dim3(kGrBlock), 0, s, in.cnt, in.nkeys, k, nfull, bc);
+    if (dev_scan(c, nfull, in.nkeys, fulloff, nf, B) != FPHE_OK) return FPHE_ERR_HIP;
+    if (dev_scan(c, bc, (size_t)k + 1, boff, nullptr, B) != FPHE_OK) return FPHE_ERR_HIP;
+    hipLaunchKernelGGL(k_gr_perm, dim3(gk), dim3(kGrBlock), 0, s, in.cnt, choff, nfull, fulloff, nf, boff, bfill,
+                       in.nkeys, k, cperm);
   }
   auto kern = in.ord ? KS<TPI>::template fold<L, int32_t, true, true>()
                      : KS<TPI>::template fold<L, int32_t, true, false>();

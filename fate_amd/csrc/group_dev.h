@@ -234,15 +234,37 @@ __global__ __launch_bounds__(kGrBlock) void k_gr_scatter_n(const int32_t* __rest
   }
 }
 
-// counting-sort keys of the chunks by length, longest first: key = klen - len (n on device)
-__global__ __launch_bounds__(kGrBlock) void k_gr_lenkeys(const int32_t* __restrict__ clen, const int32_t* __restrict__ n_dev,
-                                                         int32_t klen, int32_t* __restrict__ keys,
-                                                         int32_t* __restrict__ cnt) {
-  const size_t n = (size_t)*n_dev;
-  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x) {
-    const int32_t k = klen - clen[p];
-    keys[p] = k;
-    atomicAdd(&cnt[k], 1);
+// The order in which the fold's waves take the chunks: every full chunk (klen terms) first,
+// in key order, then each key's partial last chunk, longest first (a counting sort on the
+// remainder) -- a wave's lanes then run chunks of about equal length.  Per key: nfull[k] =
+// cnt[k] / klen, and the remainder's bucket (klen - rem) is counted in bc.
+__global__ __launch_bounds__(kGrBlock) void k_gr_permcnt(const int32_t* __restrict__ cnt, size_t nkeys, int32_t klen,
+                                                         int32_t* __restrict__ nfull, int32_t* __restrict__ bc) {
+  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < nkeys; k += (size_t)gridDim.x * blockDim.x) {
+    const int32_t c = cnt[k];
+    nfull[k] = c / klen;
+    const int32_t r = c % klen;
+    if (r) atomicAdd(&bc[klen - r], 1);
+  }
+}
+
+// cperm[fulloff[k] + i] = chunk choff[k] + i (i < nfull[k]); the partial chunk of key k goes to
+// NF + boff[bucket] + rank (NF = all full chunks, on the device)
+__global__ __launch_bounds__(kGrBlock) void k_gr_perm(const int32_t* __restrict__ cnt, const int32_t* __restrict__ choff,
+                                                      const int32_t* __restrict__ nfull,
+                                                      const int32_t* __restrict__ fulloff,
+                                                      const int32_t* __restrict__ nf_dev, const int32_t* __restrict__ boff,
+                                                      int32_t* __restrict__ bfill, size_t nkeys, int32_t klen,
+                                                      int32_t* __restrict__ cperm) {
+  const int32_t NF = *nf_dev;
+  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < nkeys; k += (size_t)gridDim.x * blockDim.x) {
+    const int32_t nfk = nfull[k], cb = choff[k], fo = fulloff[k];
+    for (int32_t i = 0; i < nfk; ++i) cperm[fo + i] = cb + i;
+    const int32_t r = cnt[k] % klen;
+    if (r) {
+      const int32_t b = klen - r;
+      cperm[NF + boff[b] + atomicAdd(&bfill[b], 1)] = cb + nfk;
+    }
   }
 }
 
