@@ -58,7 +58,7 @@ struct KeyArgs {
   const u32* ep; const u32* eq;          // n mod p(p-1), n mod q(q-1)           [L1]
   int ep_bits, eq_bits;
   const u32* KpR_27; const u32* KqR_27;  // Kp R, Kq R mod n^2 (R = 2^(LB NL2))         [NL2]
-  const u32* FR_27;                      // R^k mod n^2, k = 0..kFoldMax               [kFoldMax+1][NL2]
+  const u32* FR_27;                      // R^k mod n^2, k = 0..kFoldFR                [kFoldFR+1][NL2]
 };
 
 __device__ __forceinline__ void set_err(int32_t* err, u32 f) {
@@ -902,11 +902,10 @@ fphe_status launch_fold_segments(fphe_ctx* c, const u32* Src, const u8* ssign, c
   int32_t* cntR = B.get<int32_t>(nkeys * R);
   int32_t* offR = B.get<int32_t>(nkeys * R);
   int32_t* fill = B.get<int32_t>(nkeys * R);
-  int32_t* cnt = B.get<int32_t>(nkeys);
-  int32_t* off = B.get<int32_t>(nkeys);
   int32_t* last = B.get<int32_t>(nseg);
   u8* litseg = B.get<u8>(nseg);
   int32_t* ord = B.get<int32_t>(T);
+  int32_t* skey = B.get<int32_t>(T);
   if (!B.ok) return FPHE_ERR_HIP;
   hipLaunchKernelGGL(k_tiles_to_rows<L>, dim3((unsigned)std::min<size_t>(ntiles_of(nsrc), (size_t)c->cus * 8)),
                      dim3(kGrBlock), 0, s, Src, nsrc, rows);
@@ -917,13 +916,54 @@ fphe_status launch_fold_segments(fphe_ctx* c, const u32* Src, const u8* ssign, c
   hipLaunchKernelGGL(k_gr_keys, dim3(gr_grid(T, c->cus)), dim3(kGrBlock), 0, s, idx, seg, sexp, T, h[0], (int32_t)NE,
                      R, keys, cntR);
   if (dev_scan(c, cntR, nkeys * R, offR, nullptr, B) != FPHE_OK) return FPHE_ERR_HIP;
-  hipLaunchKernelGGL(k_gr_keysum, dim3(gr_grid(nkeys, c->cus)), dim3(kGrBlock), 0, s, cntR, offR, nkeys, R, cnt, off);
-  hipLaunchKernelGGL(k_gr_scatter, dim3(gr_grid(T, c->cus)), dim3(kGrBlock), 0, s, keys, idx, T, R, offR, fill, ord);
-  // 4. fold every (segment, exponent) run to one partial
+  hipLaunchKernelGGL(k_gr_scatter, dim3(gr_grid(T, c->cus)), dim3(kGrBlock), 0, s, keys, idx, T, R, offR, fill, ord,
+                     skey);
+  // 4. fold every (segment, exponent) run to one partial.  First level: the sorted items in
+  // equal ranges of r per wave slot, whatever the runs (k_segfold27: balanced, a whole number
+  // of wave rounds); then chunk levels per key until one partial is left per key.
+  auto ksf = KS<TPI>::template segfold<L, true>();
+  const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
+  set_lds(ksf, lds);
+  const size_t round = (size_t)occ_grid(c, ksf, lds, (size_t)1 << 40, "segfold") * kWavesPerBlock * E;
+  size_t r = (T + round - 1) / round;
+  r = r < 8 ? 8 : (r > (size_t)kFoldFR ? (size_t)kFoldFR : r);
+  const size_t nslots = (T + r - 1) / r;
+  int32_t* pcnt = B.get<int32_t>(nslots);
+  int32_t* poff = B.get<int32_t>(nslots);
+  int32_t* cnt2 = B.get<int32_t>(nkeys);
+  int32_t* off2 = B.get<int32_t>(nkeys);
+  int32_t* tmp = B.get<int32_t>(nkeys);
+  int32_t* hdr = B.get<int32_t>(4);
+  if (!B.ok) return FPHE_ERR_HIP;
+  if (hipMemsetAsync(cnt2, 0, nkeys * 4, s) != hipSuccess || hipMemsetAsync(hdr, 0, 16, s) != hipSuccess)
+    return FPHE_ERR_HIP;
+  hipLaunchKernelGGL(k_gr_segcount, dim3(gr_grid(nslots, c->cus)), dim3(kGrBlock), 0, s, skey, T, (u32)r, pcnt, cnt2);
+  if (dev_scan(c, pcnt, nslots, poff, hdr + 2, B) != FPHE_OK || dev_scan(c, cnt2, nkeys, off2, nullptr, B) != FPHE_OK)
+    return FPHE_ERR_HIP;
+  hipLaunchKernelGGL(k_gr_nchunks, dim3(gr_grid(nkeys, c->cus)), dim3(kGrBlock), 0, s, cnt2, nkeys, 1, tmp, hdr);
+  if (hipMemcpyAsync(h, hdr, sizeof(h), hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+    return FPHE_ERR_HIP;
+  const size_t nnz = (size_t)h[1];  // non-empty (segment, exponent) keys
+  const size_t ub1 = nslots + nnz;
   FoldOut P{};
-  FoldLevel lv1{rows, ssign, sexp, ord, cnt, off, nkeys, T, (int32_t)T, std::min(nkeys, T)};
-  if (fold_runs<L>(c, lv1, P, B, true) != FPHE_OK) return FPHE_ERR_HIP;
-  const size_t nnz = std::min(nkeys, T);  // bound of the non-empty (segment, exponent) keys
+  P.rows = B.get<u32>(ub1 * L);
+  P.sign = B.get<u8>(ub1);
+  P.exp = B.get<int32_t>(ub1);
+  P.key = B.get<int32_t>(ub1);
+  if (!B.ok) return FPHE_ERR_HIP;
+  hipLaunchKernelGGL(ksf, dim3(occ_grid(c, ksf, lds, (nslots + E - 1) / E, "segfold")), dim3(kBlock), lds, s, c->K,
+                     rows, ssign, sexp, ord, skey, T, (u32)r, poff, c->K.FR_27, P.rows, P.sign, P.exp, P.key, (u32)NL);
+  P.cnt = cnt2;
+  P.off = off2;
+  P.n_dev = hdr + 2;
+  P.n_ub = ub1;
+  P.maxcnt = h[0];
+  if (P.maxcnt > 1) {
+    FoldOut Q{};
+    FoldLevel lv{P.rows, P.sign, P.exp, nullptr, cnt2, off2, nkeys, ub1, P.maxcnt, nnz};
+    if (fold_runs<L>(c, lv, Q, B, false) != FPHE_OK) return FPHE_ERR_HIP;
+    P = Q;
+  }
   // 5. merge each segment's per-exponent partials: align to the segment's least exponent, fold
   if (NE > 1) {
     const size_t np = P.n_ub;  // partials (bound); the exact count is P.n_dev
@@ -960,7 +1000,6 @@ fphe_status launch_fold_segments(fphe_ctx* c, const u32* Src, const u8* ssign, c
     if (dev_scan(c, gc, ng, go, nullptr, B) != FPHE_OK) return FPHE_ERR_HIP;
     hipLaunchKernelGGL(k_gr_scatter_n, dim3(gp), dim3(kGrBlock), 0, s, gk, P.n_dev, go, gf, gord);
     auto ka = KS<TPI>::template align_rows<L>();
-    const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
     set_lds(ka, lds);
     const unsigned ga = occ_grid(c, ka, lds, (np + E - 1) / E, "align_rows");
     hipLaunchKernelGGL(ka, dim3(ga), dim3(kBlock), lds, s, c->K, P.rows, P.sign, gap, gord, P.n_dev, tile_ctr,
@@ -1419,14 +1458,14 @@ fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, 
     const size_t o_N2_27 = put(to27(N2, NL2, LB2), NL2);
     const size_t o_N2R1_27 = put(to27(hbn::pow2_mod((size_t)LB2 * NL2, N2), NL2, LB2), NL2);
     const size_t o_N2R2_27 = put(to27(hbn::pow2_mod((size_t)2 * LB2 * NL2, N2), NL2, LB2), NL2);
-    // R^k mod n^2, k = 0..kFoldMax (27-bit limbs): the k_fold27 fix-up factors
+    // R^k mod n^2, k = 0..kFoldFR (28-bit limbs): the fold kernels' fix-up factors
     size_t o_FR = 0;
     {
       // rows of exactly NL2 limbs, back to back (k_fold27 indexes row k at k * NL): one put,
       // since put() pads each section to 16 bytes and NL2 = 74 is not a multiple of 4
       const Limbs R27 = hbn::pow2_mod((size_t)LB2 * NL2, N2);
       Limbs x{1}, rows;
-      for (int k = 0; k <= kFoldMax; ++k) {
+      for (int k = 0; k <= kFoldFR; ++k) {
         const Limbs r = to27(x, NL2, LB2);
         rows.insert(rows.end(), r.begin(), r.end());
         x = hbn::mod(hbn::mul(x, R27), N2);

@@ -86,18 +86,6 @@ __global__ __launch_bounds__(kGrBlock) void k_gr_keys(const int32_t* __restrict_
   }
 }
 
-// per key: the copies' total and the first copy's offset
-__global__ __launch_bounds__(kGrBlock) void k_gr_keysum(const int32_t* __restrict__ cntR, const int32_t* __restrict__ offR,
-                                                        size_t nkeys, int32_t R, int32_t* __restrict__ cnt,
-                                                        int32_t* __restrict__ off) {
-  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < nkeys; k += (size_t)gridDim.x * blockDim.x) {
-    int32_t c = 0;
-    for (int r = 0; r < R; ++r) c += cntR[k * R + r];
-    cnt[k] = c;
-    off[k] = offR[k * R];
-  }
-}
-
 // last[seg] = the position of the segment's last term, for the segments flagged in litseg
 // only (a fold that ends as the literal 1 takes its last term's exponent: the reference's
 // sequential fold ends on that term, lib.rs:303-308); other segments cost one flag read
@@ -215,11 +203,14 @@ __global__ __launch_bounds__(kGrBlock) void k_scan_add(int32_t* __restrict__ out
 // term's copy c: the order within a key is arbitrary, the fold does not depend on it)
 __global__ __launch_bounds__(kGrBlock) void k_gr_scatter(const int32_t* __restrict__ keys, const int32_t* __restrict__ idx,
                                                          size_t T, int32_t R, const int32_t* __restrict__ off,
-                                                         int32_t* __restrict__ fill, int32_t* __restrict__ ord) {
+                                                         int32_t* __restrict__ fill, int32_t* __restrict__ ord,
+                                                         int32_t* __restrict__ skey) {
   for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < T; t += (size_t)gridDim.x * blockDim.x) {
-    const size_t kc = (size_t)keys[t] * R + ((t >> kCopyShift) % R);
+    const int32_t k = keys[t];
+    const size_t kc = (size_t)k * R + ((t >> kCopyShift) % R);
     const int32_t pos = off[kc] + atomicAdd(&fill[kc], 1);
     ord[pos] = idx ? idx[t] : (int32_t)t;
+    if (skey) skey[pos] = k;
   }
 }
 
@@ -265,6 +256,28 @@ __global__ __launch_bounds__(kGrBlock) void k_gr_perm(const int32_t* __restrict_
       const int32_t b = klen - r;
       cperm[NF + boff[b] + atomicAdd(&bfill[b], 1)] = cb + nfk;
     }
+  }
+}
+
+// The balanced first level's bookkeeping: slot i covers sorted items [i r, min((i+1) r, T));
+// pcnt[i] = partials it emits (1 + run changes inside its range), cnt2[key] += 1 per run
+// piece (the next level's per-key item counts).
+__global__ __launch_bounds__(kGrBlock) void k_gr_segcount(const int32_t* __restrict__ skey, size_t T, u32 r,
+                                                          int32_t* __restrict__ pcnt, int32_t* __restrict__ cnt2) {
+  const size_t nslots = (T + r - 1) / r;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nslots; i += (size_t)gridDim.x * blockDim.x) {
+    const size_t p0 = i * r, p1 = p0 + r < T ? p0 + r : T;
+    int32_t k = skey[p0], np = 1;
+    for (size_t p = p0 + 1; p < p1; ++p) {
+      const int32_t kp = skey[p];
+      if (kp != k) {
+        atomicAdd(&cnt2[k], 1);
+        k = kp;
+        ++np;
+      }
+    }
+    atomicAdd(&cnt2[k], 1);
+    pcnt[i] = np;
   }
 }
 

@@ -26,7 +26,7 @@ REMARKS = os.path.join(ROOT, "fate_amd", "build", "kernel_resources.txt")
 # kernel name fragment -> the least occupancy (waves/SIMD) it must keep
 OCCUPANCY = {
     "k_encrypt27": 3, "k_pow_half27": 3, "k_add27": 3, "k_mul27": 3, "k_sqmul27": 3, "k_align27": 3,
-    "k_fold27": 2, "k_encrypt_crt27": 2, "k_inv_lift27": 2, "k_binv_pre27": 2, "k_binv_post27": 2,
+    "k_fold27": 2, "k_segfold27": 2, "k_align_rows27": 3, "k_encrypt_crt27": 2, "k_inv_lift27": 2, "k_binv_pre27": 2, "k_binv_post27": 2,
     "k_inv_n27": 1,
 }
 
