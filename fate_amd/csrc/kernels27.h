@@ -32,6 +32,17 @@
 #define FPHE_FOLD_PF 1
 #endif
 #define FPHE_OCC_MISC __attribute__((amdgpu_waves_per_eu(FPHE_MISC_OCC)))
+// ct-add: both operands held in registers across the alignment squarings (read once, no
+// copy-through re-reads for literal 1s), at the 2-wave register budget: same-box A/B
+// (profiles/r03/r03n_ab_add.txt) 7.58 ms per 2^20 against 7.90 at 3 waves with the re-reads
+// (92 dwords spilled there), HBM traffic 5.8 KB/element against 12.9
+#ifndef FPHE_ADD_KEEPY
+#define FPHE_ADD_KEEPY 1
+#endif
+#ifndef FPHE_ADD_OCC
+#define FPHE_ADD_OCC 2
+#endif
+#define FPHE_OCC_ADD __attribute__((amdgpu_waves_per_eu(FPHE_ADD_OCC)))
 #define FPHE_OCC_FOLD __attribute__((amdgpu_waves_per_eu(FPHE_FOLD_OCC)))
 #define FPHE_OCC_ENC __attribute__((amdgpu_waves_per_eu(FPHE_ENC_OCC)))
 // code-shape switches of the vector-op kernels (A/B and fault bisection):

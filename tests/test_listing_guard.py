@@ -8,7 +8,8 @@ compile, so the listing is the code that was assembled into the library).
    (DESIGN.md §3).  The kernels never pick a descriptor per lane, so any loop is a regression.
 2. No fused-row clobber reads (tools/wfcheck.py).
 3. Register budgets: every Montgomery-engine kernel keeps the occupancy it is built for
-   (3 waves/SIMD = <= 168 VGPRs for the modexp and vector-op kernels, 2 for the fold), and
+   (3 waves/SIMD = <= 168 VGPRs for the modexp and vector-op kernels, 2 for the fold and
+   the ct-add, which holds both operands across its squarings), and
    no kernel uses dynamic stack.
 """
 import os
@@ -25,7 +26,7 @@ REMARKS = os.path.join(ROOT, "fate_amd", "build", "kernel_resources.txt")
 
 # kernel name fragment -> the least occupancy (waves/SIMD) it must keep
 OCCUPANCY = {
-    "k_encrypt27": 3, "k_pow_half27": 3, "k_add27": 3, "k_mul27": 3, "k_sqmul27": 3, "k_align27": 3,
+    "k_encrypt27": 3, "k_pow_half27": 3, "k_add27": 2, "k_mul27": 3, "k_sqmul27": 3, "k_align27": 3,
     "k_fold27": 2, "k_segfold27": 2, "k_align_rows27": 3, "k_encrypt_crt27": 2, "k_inv_lift27": 2, "k_binv_pre27": 2, "k_binv_post27": 2,
     "k_inv_n27": 1,
 }

@@ -55,10 +55,13 @@ __device__ __forceinline__ void body(L27& A, L27& B, u32* bcol, u32 qoff, const 
       mont_mul<TPI>(A, bcol, N, np, q);
     }
   } else {
+    // MODE 3: a wave's 16 elements read 16 consecutive rows (one random block per step);
+    // MODE 4: every element reads its own random row (the fold's real gather pattern)
     u32 W[NW];
-    u32 h = seed * 2654435761u;
+    u32 h = seed * 2654435761u + (MODE == 4 ? (u32)((threadIdx.x & 63) / TPI) * 40503u : 0u);
     auto nxt = [&]() -> size_t {
       h = h * 1664525u + 1013904223u;
+      if constexpr (MODE == 4) return (size_t)((h >> 8) % (u32)nrows);
       return (size_t)(__builtin_amdgcn_readfirstlane(h) % (u32)(nrows / E)) * E + (threadIdx.x & 63) / TPI;
     };
     fetch(nxt(), W);
@@ -151,5 +154,7 @@ int main(int argc, char** argv) {
   run<2, 3>("mulslot", dN, np, io, rows, nrows, cus, iters);
   run<3, 2>("fold", dN, np, io, rows, nrows, cus, iters);
   run<3, 3>("fold", dN, np, io, rows, nrows, cus, iters);
+  run<4, 2>("foldrnd", dN, np, io, rows, nrows, cus, iters);
+  run<4, 3>("foldrnd", dN, np, io, rows, nrows, cus, iters);
   return 0;
 }
