@@ -894,8 +894,10 @@ fphe_status launch_fold_segments(fphe_ctx* c, const u32* Src, const u8* ssign, c
   const int64_t NE = (int64_t)h[1] - h[0] + 1;
   if (NE < 1 || (size_t)NE * nseg > kMaxFoldKeys) return FPHE_ERR_RANGE;
   const size_t nkeys = (size_t)NE * nseg;
-  // counter copies against atomic contention on hot keys (k_gr_keys), while they stay small
-  const int32_t R = nkeys <= ((size_t)1 << 22) ? 8 : 1;
+  // small key spaces: per-block LDS counts (k_gr_bkeys / k_gr_bscatter); larger ones: counter
+  // copies against atomic contention on hot keys (k_gr_keys), while they stay small
+  const bool lds_counts = nkeys <= kBcMaxKeys;
+  const int32_t R = lds_counts ? 1 : (nkeys <= ((size_t)1 << 22) ? 8 : 1);
   // 2. element-major copy of the source (the fold gathers whole rows)
   u32* rows = B.get<u32>(nsrc * L);
   int32_t* keys = B.get<int32_t>(T);
@@ -913,11 +915,24 @@ fphe_status launch_fold_segments(fphe_ctx* c, const u32* Src, const u8* ssign, c
   if (hipMemsetAsync(cntR, 0, nkeys * R * 4, s) != hipSuccess || hipMemsetAsync(fill, 0, nkeys * R * 4, s) != hipSuccess ||
       hipMemsetAsync(last, 0xff, nseg * 4, s) != hipSuccess || hipMemsetAsync(litseg, 0, nseg, s) != hipSuccess)
     return FPHE_ERR_HIP;
-  hipLaunchKernelGGL(k_gr_keys, dim3(gr_grid(T, c->cus)), dim3(kGrBlock), 0, s, idx, seg, sexp, T, h[0], (int32_t)NE,
-                     R, keys, cntR);
+  const unsigned nbc = (unsigned)((T + kBcTerms - 1) / kBcTerms);
+  if (lds_counts) {
+    set_lds(k_gr_bkeys, nkeys * 4);
+    set_lds(k_gr_bscatter, nkeys * 4);
+  }
+  if (lds_counts)
+    hipLaunchKernelGGL(k_gr_bkeys, dim3(nbc), dim3(kGrBlock), nkeys * 4, s, idx, seg, sexp, T, h[0], (int32_t)NE,
+                       (int32_t)nkeys, keys, cntR);
+  else
+    hipLaunchKernelGGL(k_gr_keys, dim3(gr_grid(T, c->cus)), dim3(kGrBlock), 0, s, idx, seg, sexp, T, h[0], (int32_t)NE,
+                       R, keys, cntR);
   if (dev_scan(c, cntR, nkeys * R, offR, nullptr, B) != FPHE_OK) return FPHE_ERR_HIP;
-  hipLaunchKernelGGL(k_gr_scatter, dim3(gr_grid(T, c->cus)), dim3(kGrBlock), 0, s, keys, idx, T, R, offR, fill, ord,
-                     skey);
+  if (lds_counts)
+    hipLaunchKernelGGL(k_gr_bscatter, dim3(nbc), dim3(kGrBlock), nkeys * 4, s, keys, idx, T, (int32_t)nkeys, offR, fill,
+                       ord, skey);
+  else
+    hipLaunchKernelGGL(k_gr_scatter, dim3(gr_grid(T, c->cus)), dim3(kGrBlock), 0, s, keys, idx, T, R, offR, fill, ord,
+                       skey);
   // 4. fold every (segment, exponent) run to one partial.  First level: the sorted items in
   // equal ranges of r per wave slot, whatever the runs (k_segfold27: balanced, a whole number
   // of wave rounds); then chunk levels per key until one partial is left per key.

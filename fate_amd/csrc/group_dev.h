@@ -86,6 +86,37 @@ __global__ __launch_bounds__(kGrBlock) void k_gr_keys(const int32_t* __restrict_
   }
 }
 
+// The same pass with the counts aggregated per block in LDS (key spaces up to kBcMaxKeys):
+// block b owns terms [b kBcTerms, (b + 1) kBcTerms), counts them with LDS atomics and adds each
+// non-zero count to cnt[key] once -- a few global atomics per key and block instead of one per
+// term.  k_gr_bscatter is its scatter.
+constexpr int kBcItems = 16;
+constexpr int kBcTerms = kGrBlock * kBcItems;
+constexpr size_t kBcMaxKeys = 16384;  // 64 KB of LDS counters
+__global__ __launch_bounds__(kGrBlock) void k_gr_bkeys(const int32_t* __restrict__ idx, const int32_t* __restrict__ seg,
+                                                       const int32_t* __restrict__ sexp, size_t T, int32_t emin, int32_t NE,
+                                                       int32_t nkeys, int32_t* __restrict__ keys, int32_t* __restrict__ cnt) {
+  extern __shared__ int32_t hist[];
+  for (int32_t k = threadIdx.x; k < nkeys; k += kGrBlock) hist[k] = 0;
+  __syncthreads();
+  const size_t t0 = (size_t)blockIdx.x * kBcTerms + threadIdx.x;
+#pragma unroll 4
+  for (int i = 0; i < kBcItems; ++i) {
+    const size_t t = t0 + (size_t)i * kGrBlock;
+    if (t < T) {
+      const int32_t src = idx ? idx[t] : (int32_t)t;
+      const int32_t k = seg[t] * NE + (sexp[src] - emin);
+      keys[t] = k;
+      atomicAdd(&hist[k], 1);
+    }
+  }
+  __syncthreads();
+  for (int32_t k = threadIdx.x; k < nkeys; k += kGrBlock) {
+    const int32_t c = hist[k];
+    if (c) atomicAdd(&cnt[k], c);
+  }
+}
+
 // last[seg] = the position of the segment's last term, for the segments flagged in litseg
 // only (a fold that ends as the literal 1 takes its last term's exponent: the reference's
 // sequential fold ends on that term, lib.rs:303-308); other segments cost one flag read
@@ -211,6 +242,40 @@ __global__ __launch_bounds__(kGrBlock) void k_gr_scatter(const int32_t* __restri
     const int32_t pos = off[kc] + atomicAdd(&fill[kc], 1);
     ord[pos] = idx ? idx[t] : (int32_t)t;
     if (skey) skey[pos] = k;
+  }
+}
+
+// k_gr_bkeys' scatter: each term's rank within its block and key from an LDS atomic, one global
+// cursor reservation per non-zero (block, key), then ord[off[key] + base + rank]
+__global__ __launch_bounds__(kGrBlock) void k_gr_bscatter(const int32_t* __restrict__ keys, const int32_t* __restrict__ idx,
+                                                          size_t T, int32_t nkeys, const int32_t* __restrict__ off,
+                                                          int32_t* __restrict__ fill, int32_t* __restrict__ ord,
+                                                          int32_t* __restrict__ skey) {
+  extern __shared__ int32_t hist[];
+  for (int32_t k = threadIdx.x; k < nkeys; k += kGrBlock) hist[k] = 0;
+  __syncthreads();
+  const size_t t0 = (size_t)blockIdx.x * kBcTerms + threadIdx.x;
+  int32_t kk[kBcItems], rk[kBcItems];
+#pragma unroll
+  for (int i = 0; i < kBcItems; ++i) {
+    const size_t t = t0 + (size_t)i * kGrBlock;
+    kk[i] = t < T ? keys[t] : -1;
+  }
+#pragma unroll
+  for (int i = 0; i < kBcItems; ++i) rk[i] = kk[i] >= 0 ? atomicAdd(&hist[kk[i]], 1) : 0;
+  __syncthreads();
+  for (int32_t k = threadIdx.x; k < nkeys; k += kGrBlock) {
+    const int32_t c = hist[k];
+    if (c) hist[k] = off[k] + atomicAdd(&fill[k], c);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kBcItems; ++i) {
+    if (kk[i] < 0) continue;
+    const size_t t = t0 + (size_t)i * kGrBlock;
+    const int32_t pos = hist[kk[i]] + rk[i];
+    ord[pos] = idx ? idx[t] : (int32_t)t;
+    if (skey) skey[pos] = kk[i];
   }
 }
 

@@ -798,7 +798,8 @@ class CiphertextVector:
         slot = (pp[:, None] * stride + t).reshape(-1)
         # one ciphertext per slot (the literal 1 where no term lands: add's identity), then
         # data[s] = add(data[s], fold(terms of s)) for every slot at once
-        folded, present = _fold_to_segments(pk, other, slot, self.count, index=src, with_present=True)
+        errs = []  # read back after the add is queued: the host work overlaps the fold's tail
+        folded, present = _fold_to_segments(pk, other, slot, self.count, index=src, with_present=True, deferred=errs)
         cur = _fit_limbs(self, pk._key.L2)
         r = _add(pk, cur, folded, broadcast=False)
         # slots no term reaches keep their value as it was (exponent of a literal 1 included:
@@ -807,6 +808,8 @@ class CiphertextVector:
         r.C = torch.where(keep.view(-1, 1, WAVE), cur.C, r.C)
         r.sign = torch.where(keep, cur.sign, r.sign)
         r.exp = torch.where(keep, cur.exp, r.exp)
+        for e in errs:
+            _fold_check(e)
         self.C, self.sign, self.exp = r.C, r.sign, r.exp
 
     def chunking_cumsum_with_step(self, pk: "PK", chunk_sizes: Sequence[int], step: int) -> None:
@@ -1080,13 +1083,21 @@ def _fold_segments(pk: "PK", src: CiphertextVector, seg: torch.Tensor, index: Op
     return res, ids
 
 
+def _fold_check(err: torch.Tensor) -> None:
+    """Raise on the device error flags of a fold (reads them back: synchronises)."""
+    if int(err.item()) & _lib.EF_EXP_RANGE:
+        raise ValueError(f"exponent gap beyond {MAX_GAP} in a fold: corrupt exponents")
+
+
 def _fold_to_segments(pk: "PK", src: CiphertextVector, seg: torch.Tensor, nseg: int,
-                      index: Optional[torch.Tensor] = None, with_present: bool = False):
+                      index: Optional[torch.Tensor] = None, with_present: bool = False, deferred: list = None):
     """out[s] = the reference's sequential ct-add fold of the terms src[index[t]] with seg[t] == s,
     for every s < nseg (the literal 1, exp 0, where no term lands) -- fphe_fold_segments, which
     groups, folds and merges the exponents on the device.  Falls back to the torch grouping of
     :func:`_fold_segments` when the (segment, exponent) key space is too large for it.
-    with_present: also return the per-segment uint8 flags "some term landed here"."""
+    with_present: also return the per-segment uint8 flags "some term landed here".
+    deferred: a list to append the device error flags to instead of reading them back here
+    (the caller then calls :func:`_fold_check` once its follow-up launches are queued)."""
     dev = src.device
     src = _fit_limbs(src, pk._key.L2)
     L2 = pk._key.L2
@@ -1116,8 +1127,10 @@ def _fold_to_segments(pk: "PK", src: CiphertextVector, seg: torch.Tensor, nseg: 
     if st == _lib.FPHE_ERR_ARG:
         raise PanicException("index out of bounds")
     _lib.check(st, "fphe_fold_segments")
-    if int(err.item()) & _lib.EF_EXP_RANGE:
-        raise ValueError(f"exponent gap beyond {MAX_GAP} in a fold: corrupt exponents")
+    if deferred is not None:
+        deferred.append(err)
+    else:
+        _fold_check(err)
     return (out, present) if with_present else out
 
 

@@ -101,6 +101,20 @@ def test_fold_segments_identity_index_and_fallback(env):
     assert host(pk, got) == oracle_fold(opk, far, list(range(len(far))), segf, 1400)
 
 
+def test_fold_segments_large_key_space(env):
+    """(segment, exponent) key spaces past the per-block LDS counters (16384 keys: the global
+    counter-copy path of the counting sort) and just inside them, against the oracle."""
+    fx, sk, pk, coder, opk, cts = env
+    src = mixed_sources(opk, cts, 200, 13)  # exponents -40 .. 18: 59 per segment
+    rng = random.Random(13)
+    for nseg in (270, 300):  # 15,930 and 17,700 keys
+        T = 900
+        idx = [rng.randrange(len(src)) for _ in range(T)]
+        seg = [rng.randrange(nseg) for _ in range(T)]
+        got = P._fold_to_segments(pk, dev_vec(pk, src), torch.tensor(seg), nseg, index=torch.tensor(idx))
+        assert host(pk, got) == oracle_fold(opk, src, idx, seg, nseg)
+
+
 def test_fold_segments_bad_index_panics(env):
     fx, sk, pk, coder, opk, cts = env
     v = dev_vec(pk, more(opk, cts, 10))

@@ -6,6 +6,8 @@ T=${1:-segpmc}
 cd $R && mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_ops.py tests/test_gpu_fold.py tests/test_gpu_edges.py -k "add or fold or chain or literal or iupdate" > gpurun_out/${T}_tests.txt 2>&1 || { echo tests_failed; tail -40 gpurun_out/${T}_tests.txt; exit 1; }
 tail -3 gpurun_out/${T}_tests.txt
+timeout -k 10 120 tools/probe/mulsq_probe 300 1 > gpurun_out/${T}_probe_rnd.txt 2>&1 || { echo probe_failed; exit 1; }
+cat gpurun_out/${T}_probe_rnd.txt
 cd /tmp && export TMPDIR=/tmp
 P1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM"
 P2="SQ_INSTS_SALU SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_BRANCH SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_INSTS_VALU"

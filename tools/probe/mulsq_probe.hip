@@ -100,6 +100,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
   for (int j = 0; j < LL; ++j) io[base + j] = A[j];
 }
 
+// random 28-bit-safe words (a hash of the index): data-dependent power is part of what a real
+// operand stream costs, so the probe does not run on a constant pattern
+__global__ void k_fill(u32* p, size_t n, u32 salt) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    u32 h = (u32)i * 2654435761u ^ salt;
+    h ^= h >> 15; h *= 2246822519u; h ^= h >> 13; h *= 3266489917u; h ^= h >> 16;
+    p[i] = h;
+  }
+}
+
 template <int MODE, int OCC>
 void run(const char* name, const u32* dN, u32 np, u32* io, const u32* rows, size_t nrows, int cus, int iters) {
   const int blocks = cus * OCC;  // 4 waves per block, OCC blocks per CU = OCC waves per SIMD
@@ -144,8 +154,16 @@ int main(int argc, char** argv) {
   (void)hipMalloc(&io, n * 4);
   (void)hipMalloc(&rows, nrows * 128 * 4);
   (void)hipMemcpy(dN, hN, NL * 4, hipMemcpyHostToDevice);
-  (void)hipMemset(io, 0x5a, n * 4);
-  (void)hipMemset(rows, 0x33, nrows * 128 * 4);
+  const bool rnd = argc > 2 && atoi(argv[2]) != 0;
+  if (rnd) {
+    hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, io, n, 0x1234u);
+    hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, rows, nrows * 128, 0x9876u);
+    (void)hipDeviceSynchronize();
+  } else {
+    (void)hipMemset(io, 0x5a, n * 4);
+    (void)hipMemset(rows, 0x33, nrows * 128 * 4);
+  }
+  printf("operands: %s\n", rnd ? "random" : "constant pattern");
   run<0, 2>("sq", dN, np, io, rows, nrows, cus, iters);
   run<0, 3>("sq", dN, np, io, rows, nrows, cus, iters);
   run<1, 2>("mul", dN, np, io, rows, nrows, cus, iters);
