@@ -26,7 +26,11 @@ namespace {
 constexpr int kBlock = 256;      // 4 waves per workgroup
 constexpr int kWavesPerBlock = kBlock / FPHE_WAVE;
 constexpr int kWinSlide = 6;     // sliding window of the 27-bit engine's shared-exponent modexps
-constexpr int kWinMul = 4;       // window of the per-lane-exponent modexp (ct x pt)
+constexpr int kWinMul = 4;       // window of the per-lane-exponent modexp (ct x pt): table capacity
+#ifndef FPHE_MUL_ADAPT
+#define FPHE_MUL_ADAPT 1  // ct x pt: 3-bit window for short exponents, all-zero windows skipped
+#endif
+constexpr int kMulShortBits = 64;  // waves whose longest exponent fits this take a 3-bit window
 
 // Uniform key material, passed by value (lands in the kernarg segment -> SGPRs).
 struct KeyArgs {
