@@ -35,7 +35,7 @@ EXPORTED_SYMBOLS = (
     "fphe_ctx_create", "fphe_ctx_destroy", "fphe_ctx_limbs",
     "fphe_encode_f32", "fphe_encode_f64", "fphe_decode_f32", "fphe_decode_f64",
     "fphe_encode_i64", "fphe_decode_i64", "fphe_decode_i32", "fphe_pack_f64", "fphe_unpack_f64",
-    "fphe_encrypt", "fphe_encrypt_crt", "fphe_decrypt", "fphe_add", "fphe_add_ordered", "fphe_mul", "fphe_neg", "fphe_sqmul", "fphe_align",
+    "fphe_encrypt", "fphe_encrypt_crt", "fphe_decrypt", "fphe_add", "fphe_add_ordered", "fphe_add_order", "fphe_mul", "fphe_neg", "fphe_sqmul", "fphe_align",
     "fphe_fold", "fphe_fold_segments", "fphe_permute", "fphe_export_signed", "fphe_import_signed",
     "fphe_wire_lengths", "fphe_wire_encode", "fphe_wire_scan", "fphe_wire_decode", "fphe_chacha20_blocks",
 )
@@ -115,6 +115,9 @@ def load() -> ctypes.CDLL:
         lib.fphe_fold_segments.argtypes = [vp, vp, vp, vp, ctypes.c_size_t, vp, vp, ctypes.c_size_t, ctypes.c_size_t,
                                            vp, vp, vp, vp, vp, vp]
         lib.fphe_fold_segments.restype = st
+        if hasattr(lib, "fphe_add_order"):  # an A/B build from before it (FPHE_LIB_PATH) lacks it
+            lib.fphe_add_order.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_uint32, vp, vp]
+            lib.fphe_add_order.restype = st
         lib.fphe_permute.argtypes = [vp, vp, vp, ctypes.c_uint32, vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int,
                                      vp, vp, vp, vp]
         lib.fphe_permute.restype = st

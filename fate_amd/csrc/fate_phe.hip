@@ -30,7 +30,9 @@ constexpr int kWinMul = 4;       // window of the per-lane-exponent modexp (ct x
 #ifndef FPHE_MUL_ADAPT
 #define FPHE_MUL_ADAPT 1  // ct x pt: 3-bit window for short exponents, all-zero windows skipped
 #endif
-constexpr int kMulShortBits = 64;  // waves whose longest exponent fits this take a 3-bit window
+constexpr int kMulShortBits = 64;
+constexpr u32 kAddRegions = 8;          // k_add27: one run of wave tiles per XCD (blocks b, b + 8, ...)
+constexpr u32 kAddCounterStride = 32;   // the runs' tile counters, 128 B apart  // waves whose longest exponent fits this take a 3-bit window
 
 // Uniform key material, passed by value (lands in the kernarg segment -> SGPRs).
 struct KeyArgs {
@@ -1058,13 +1060,16 @@ fphe_status launch_add27(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, con
   if (ord && count > cmax) return FPHE_ERR_ARG;  // an order must stay inside one addressable chunk
   if (count == 0) return FPHE_OK;
   // the kernel's wave-tile counter lives in the context scratch (stream-owned, see ensure_scratch)
-  if (ensure_scratch(c, 256, s) != FPHE_OK) return FPHE_ERR_HIP;
+  constexpr size_t kCtrBytes = (size_t)kAddRegions * kAddCounterStride * 4;
+  if (ensure_scratch(c, kCtrBytes, s) != FPHE_OK) return FPHE_ERR_HIP;
   u32* next_tile = c->scratch;
   for (size_t s0 = 0; s0 < count; s0 += cmax) {  // whole tiles per chunk: pointer offsets stay tile-aligned
     const size_t n = count - s0 < cmax ? count - s0 : cmax;
     const size_t wo = s0 / FPHE_WAVE * L * FPHE_WAVE;  // word offset of the chunk's first tile
-    const unsigned grid = occ_grid(c, kern, lds, (n + E - 1) / E, "add27");
-    if (hipMemsetAsync(next_tile, 0, sizeof(u32), s) != hipSuccess) return FPHE_ERR_HIP;
+    // a multiple of kAddRegions blocks: every run of wave tiles has its own blocks
+    const unsigned g0 = occ_grid(c, kern, lds, (n + E - 1) / E, "add27");
+    const unsigned grid = (g0 + kAddRegions - 1) / kAddRegions * kAddRegions;
+    if (hipMemsetAsync(next_tile, 0, kCtrBytes, s) != hipSuccess) return FPHE_ERR_HIP;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, Ca + wo, sa + s0, ea + s0,
                        bstride ? Cb + wo : Cb, bstride ? sb + s0 : sb, bstride ? eb + s0 : eb, bstride, n, ord,
                        Co + wo, so + s0, eo + s0, next_tile, (u32)NL);
@@ -1437,12 +1442,13 @@ extern "C" {
 fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, const uint32_t* p_w,
                             const uint32_t* q_w, fphe_ctx** out) {
   if (!out || !n_w) return FPHE_ERR_ARG;
-  // any even size up to 2048 bits (paillier/src/lib.rs:72-87 accepts any even size): the
-  // kernels run the 1024- or the 2048-bit geometry with n zero-padded to it (R >= 4N holds,
-  // so the lazy Montgomery bounds are unchanged)
-  if (key_bits < 256 || key_bits > 2048 || key_bits % 2) return FPHE_ERR_ARG;
+  // any even size up to 4096 bits (paillier/src/lib.rs:72-87 accepts any even size): the
+  // kernels run the 1024-, 2048- or 4096-bit geometry with n zero-padded to it (R >= 4N
+  // holds, so the lazy Montgomery bounds are unchanged).  Above 2048 bits n^2 spans 8 lanes
+  // per element (TPI 8, 296 limbs of 28 bits) and n, p^2, q^2 the TPI-4 geometry.
+  if (key_bits < 256 || key_bits > 4096 || key_bits % 2) return FPHE_ERR_ARG;
   if ((p_w == nullptr) != (q_w == nullptr)) return FPHE_ERR_ARG;
-  const int L1 = key_bits <= 1024 ? 32 : 64, L2 = 2 * L1, LQ = L1 / 2;
+  const int L1 = key_bits <= 1024 ? 32 : (key_bits <= 2048 ? 64 : 128), L2 = 2 * L1, LQ = L1 / 2;
   try {
     Limbs n = from_words(n_w, L1);
     if (n.empty() || !(n[0] & 1)) return FPHE_ERR_KEY;
@@ -1648,7 +1654,9 @@ fphe_status fphe_decode_f32(const fphe_ctx* c, const uint32_t* P, uint32_t lp, c
   if (!P || !exp || !out || lp == 0) return FPHE_ERR_ARG;
   DevGuard g(c->device);
   const unsigned grid = (unsigned)std::min<size_t>((count + 255) / 256, (size_t)c->cus * 8);
-  if (c->L1 == 64)
+  if (c->L1 == 128)
+    hipLaunchKernelGGL(k_decode_f32<128>, dim3(grid), dim3(256), 0, (hipStream_t)stream, c->K, P, lp, exp, count, out, err);
+  else if (c->L1 == 64)
     hipLaunchKernelGGL(k_decode_f32<64>, dim3(grid), dim3(256), 0, (hipStream_t)stream, c->K, P, lp, exp, count, out, err);
   else
     hipLaunchKernelGGL(k_decode_f32<32>, dim3(grid), dim3(256), 0, (hipStream_t)stream, c->K, P, lp, exp, count, out, err);
@@ -1662,7 +1670,9 @@ fphe_status fphe_decode_f64(const fphe_ctx* c, const uint32_t* P, uint32_t lp, c
   if (!P || !exp || !out || lp == 0) return FPHE_ERR_ARG;
   DevGuard g(c->device);
   const unsigned grid = (unsigned)std::min<size_t>((count + 255) / 256, (size_t)c->cus * 8);
-  if (c->L1 == 64)
+  if (c->L1 == 128)
+    hipLaunchKernelGGL(k_decode_f64<128>, dim3(grid), dim3(256), 0, (hipStream_t)stream, c->K, P, lp, exp, count, out, err);
+  else if (c->L1 == 64)
     hipLaunchKernelGGL(k_decode_f64<64>, dim3(grid), dim3(256), 0, (hipStream_t)stream, c->K, P, lp, exp, count, out, err);
   else
     hipLaunchKernelGGL(k_decode_f64<32>, dim3(grid), dim3(256), 0, (hipStream_t)stream, c->K, P, lp, exp, count, out, err);
@@ -1677,7 +1687,9 @@ fphe_status fphe_encode_i64(const fphe_ctx* c, const int64_t* x, size_t count, u
   if (!x || !P || !neg || !exp) return FPHE_ERR_ARG;
   DevGuard g(c->device);
   const unsigned grid = (unsigned)std::min<size_t>((count + 255) / 256, (size_t)c->cus * 8);
-  if (c->L1 == 64)
+  if (c->L1 == 128)
+    hipLaunchKernelGGL(k_encode_i64<128>, dim3(grid), dim3(256), 0, (hipStream_t)stream, c->K, x, count, P, neg, exp);
+  else if (c->L1 == 64)
     hipLaunchKernelGGL(k_encode_i64<64>, dim3(grid), dim3(256), 0, (hipStream_t)stream, c->K, x, count, P, neg, exp);
   else
     hipLaunchKernelGGL(k_encode_i64<32>, dim3(grid), dim3(256), 0, (hipStream_t)stream, c->K, x, count, P, neg, exp);
@@ -1691,7 +1703,9 @@ fphe_status fphe_decode_i64(const fphe_ctx* c, const uint32_t* P, uint32_t lp, c
   if (!P || !exp || !out || lp == 0) return FPHE_ERR_ARG;
   DevGuard g(c->device);
   const unsigned grid = (unsigned)std::min<size_t>((count + 255) / 256, (size_t)c->cus * 8);
-  if (c->L1 == 64)
+  if (c->L1 == 128)
+    hipLaunchKernelGGL(k_decode_i64<128>, dim3(grid), dim3(256), 0, (hipStream_t)stream, c->K, P, lp, exp, count, out, err);
+  else if (c->L1 == 64)
     hipLaunchKernelGGL(k_decode_i64<64>, dim3(grid), dim3(256), 0, (hipStream_t)stream, c->K, P, lp, exp, count, out, err);
   else
     hipLaunchKernelGGL(k_decode_i64<32>, dim3(grid), dim3(256), 0, (hipStream_t)stream, c->K, P, lp, exp, count, out, err);
@@ -1705,7 +1719,9 @@ fphe_status fphe_decode_i32(const fphe_ctx* c, const uint32_t* P, uint32_t lp, c
   if (!P || !exp || !out || lp == 0) return FPHE_ERR_ARG;
   DevGuard g(c->device);
   const unsigned grid = (unsigned)std::min<size_t>((count + 255) / 256, (size_t)c->cus * 8);
-  if (c->L1 == 64)
+  if (c->L1 == 128)
+    hipLaunchKernelGGL(k_decode_i32<128>, dim3(grid), dim3(256), 0, (hipStream_t)stream, c->K, P, lp, exp, count, out, err);
+  else if (c->L1 == 64)
     hipLaunchKernelGGL(k_decode_i32<64>, dim3(grid), dim3(256), 0, (hipStream_t)stream, c->K, P, lp, exp, count, out, err);
   else
     hipLaunchKernelGGL(k_decode_i32<32>, dim3(grid), dim3(256), 0, (hipStream_t)stream, c->K, P, lp, exp, count, out, err);
@@ -1721,7 +1737,10 @@ fphe_status fphe_pack_f64(const fphe_ctx* c, const double* x, size_t count, uint
   DevGuard g(c->device);
   const size_t nout = (count + pack_num - 1) / pack_num;
   const unsigned grid = (unsigned)std::min<size_t>((nout + 63) / 64, (size_t)c->cus * 16);
-  if (c->L1 == 64)
+  if (c->L1 == 128)
+    hipLaunchKernelGGL(k_pack_f64<128>, dim3(grid), dim3(64), 0, (hipStream_t)stream, x, count, offset_bit, pack_num,
+                       precision, nout, P, neg, exp, err);
+  else if (c->L1 == 64)
     hipLaunchKernelGGL(k_pack_f64<64>, dim3(grid), dim3(64), 0, (hipStream_t)stream, x, count, offset_bit, pack_num,
                        precision, nout, P, neg, exp, err);
   else
@@ -1737,7 +1756,10 @@ fphe_status fphe_unpack_f64(const fphe_ctx* c, const uint32_t* P, uint32_t lp, s
   if (!P || !out || lp == 0) return FPHE_ERR_ARG;
   DevGuard g(c->device);
   const unsigned grid = (unsigned)std::min<size_t>((npacked + 255) / 256, (size_t)c->cus * 8);
-  if (c->L1 == 64)
+  if (c->L1 == 128)
+    hipLaunchKernelGGL(k_unpack_f64<128>, dim3(grid), dim3(256), 0, (hipStream_t)stream, P, lp, npacked, offset_bit,
+                       pack_num, precision, total, out);
+  else if (c->L1 == 64)
     hipLaunchKernelGGL(k_unpack_f64<64>, dim3(grid), dim3(256), 0, (hipStream_t)stream, P, lp, npacked, offset_bit,
                        pack_num, precision, total, out);
   else
@@ -1756,6 +1778,8 @@ fphe_status fphe_encrypt(fphe_ctx* c, const uint32_t* P, uint32_t lp, const uint
   if (obf && !r && !rng_key) return FPHE_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DevGuard g(c->device);
+  if (c->L2 == 256)
+    return launch_encrypt27<256>(c, P, lp, neg, count, obf, r, rng_key, nonce, C, sign, (hipStream_t)stream);
   if (c->L2 == 128)
     return launch_encrypt27<128>(c, P, lp, neg, count, obf, r, rng_key, nonce, C, sign, (hipStream_t)stream);
   return launch_encrypt27<64>(c, P, lp, neg, count, obf, r, rng_key, nonce, C, sign, (hipStream_t)stream);
@@ -1773,6 +1797,8 @@ fphe_status fphe_encrypt_crt(fphe_ctx* c, const uint32_t* P, uint32_t lp, const 
   if (!r && !rng_key) return FPHE_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DevGuard g(c->device);
+  if (c->L2 == 256)
+    return launch_encrypt_crt27<256>(c, P, lp, neg, count, r, rng_key, nonce, C, sign, (hipStream_t)stream);
   if (c->L2 == 128)
     return launch_encrypt_crt27<128>(c, P, lp, neg, count, r, rng_key, nonce, C, sign, (hipStream_t)stream);
   return launch_encrypt_crt27<64>(c, P, lp, neg, count, r, rng_key, nonce, C, sign, (hipStream_t)stream);
@@ -1788,6 +1814,8 @@ fphe_status fphe_fold(fphe_ctx* c, const uint32_t* Src, const uint8_t* ssign, co
   if (nchunks >= (1ull << 32)) return FPHE_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DevGuard g(c->device);
+  if (c->L2 == 256)
+    return launch_fold27<256>(c, Src, ssign, sexp, ord, cstart, clen, nchunks, Co, so, eo, (hipStream_t)stream);
   if (c->L2 == 128)
     return launch_fold27<128>(c, Src, ssign, sexp, ord, cstart, clen, nchunks, Co, so, eo, (hipStream_t)stream);
   return launch_fold27<64>(c, Src, ssign, sexp, ord, cstart, clen, nchunks, Co, so, eo, (hipStream_t)stream);
@@ -1804,6 +1832,9 @@ fphe_status fphe_fold_segments(fphe_ctx* c, const uint32_t* Src, const uint8_t* 
   if (nterms && !idx && nsrc < nterms) return FPHE_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DevGuard g(c->device);
+  if (c->L2 == 256)
+    return launch_fold_segments<256>(c, Src, ssign, sexp, nsrc, idx, seg, nterms, nseg, Co, so, eo, present, err,
+                                     (hipStream_t)stream);
   if (c->L2 == 128)
     return launch_fold_segments<128>(c, Src, ssign, sexp, nsrc, idx, seg, nterms, nseg, Co, so, eo, present, err,
                                      (hipStream_t)stream);
@@ -1819,6 +1850,7 @@ fphe_status fphe_decrypt(fphe_ctx* c, const uint32_t* C, size_t count, uint32_t*
   if (!C || !P) return FPHE_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DevGuard g(c->device);
+  if (c->L2 == 256) return launch_decrypt27<256>(c, C, count, P, (hipStream_t)stream);
   if (c->L2 == 128) return launch_decrypt27<128>(c, C, count, P, (hipStream_t)stream);
   return launch_decrypt27<64>(c, C, count, P, (hipStream_t)stream);
 }
@@ -1832,9 +1864,32 @@ fphe_status fphe_add_ordered(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa,
   if (!Ca || !sa || !ea || !Cb || !sb || !eb || !Co || !so || !eo) return FPHE_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DevGuard g(c->device);
+  if (c->L2 == 256)
+    return launch_add27<256>(c, Ca, sa, ea, Cb, sb, eb, b_stride, count, order, Co, so, eo, (hipStream_t)stream);
   if (c->L2 == 128)
     return launch_add27<128>(c, Ca, sa, ea, Cb, sb, eb, b_stride, count, order, Co, so, eo, (hipStream_t)stream);
   return launch_add27<64>(c, Ca, sa, ea, Cb, sb, eb, b_stride, count, order, Co, so, eo, (hipStream_t)stream);
+}
+
+fphe_status fphe_add_order(const int32_t* ea, const int32_t* eb, size_t count, uint32_t L2, int32_t* order,
+                           void* stream) {
+  if (count == 0) return FPHE_OK;
+  if (!ea || !eb || !order || (L2 != 64 && L2 != 128 && L2 != 256)) return FPHE_ERR_ARG;
+  if (count >= (1ull << 31)) return FPHE_ERR_ARG;
+  static_assert(kAoRuns == (int)kAddRegions, "the order's runs are k_add27's XCD runs");
+  hipStream_t s = (hipStream_t)stream;
+  const size_t E = FPHE_WAVE / (L2 / 32), nwt = (count + E - 1) / E;
+  const size_t run = (nwt + kAoRuns - 1) / kAoRuns * E;      // elements per run (whole wave tiles)
+  const u32 nbr = (u32)((run + kAoBlock - 1) / kAoBlock);    // blocks per run
+  const u32 nblk = (u32)kAoRuns * nbr;
+  CallBufs B(s);
+  int32_t* counts = B.get<int32_t>((size_t)nblk * kAoBins);
+  int32_t* offsets = B.get<int32_t>((size_t)nblk * kAoBins);
+  if (!B.ok) return FPHE_ERR_HIP;
+  hipLaunchKernelGGL(k_ao_count, dim3(nblk), dim3(kGrBlock), 0, s, ea, eb, count, run, nbr, counts);
+  hipLaunchKernelGGL(k_ao_scan, dim3(kAoRuns), dim3(kGrBlock), 0, s, counts, run, nbr, offsets);
+  hipLaunchKernelGGL(k_ao_scatter, dim3(nblk), dim3(kGrBlock), 0, s, ea, eb, count, run, nbr, offsets, order);
+  return hip_ok(hipGetLastError());
 }
 
 fphe_status fphe_add(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, const int32_t* ea, const uint32_t* Cb,
@@ -1852,9 +1907,12 @@ fphe_status fphe_neg(fphe_ctx* c, const uint32_t* Ca, size_t count, uint32_t* Co
   DevGuard g(c->device);
   // large vectors: one inverse per group of 16 (8 at 1024 bits) elements (Montgomery's trick)
   if (count >= binv_min()) {
-    const size_t w = c->L2 == 128 ? binv_scratch_bytes<128>(count) : binv_scratch_bytes<64>(count);
+    const size_t w = c->L2 == 256 ? binv_scratch_bytes<256>(count)
+                     : c->L2 == 128 ? binv_scratch_bytes<128>(count) : binv_scratch_bytes<64>(count);
     if (ensure_scratch(c, w, (hipStream_t)stream) != FPHE_OK) return FPHE_ERR_HIP;
-    if (c->L2 == 128)
+    if (c->L2 == 256)
+      launch_binv27<256>(c, Ca, count, nullptr, Co, err, c->scratch, (hipStream_t)stream);
+    else if (c->L2 == 128)
       launch_binv27<128>(c, Ca, count, nullptr, Co, err, c->scratch, (hipStream_t)stream);
     else
       launch_binv27<64>(c, Ca, count, nullptr, Co, err, c->scratch, (hipStream_t)stream);
@@ -1862,7 +1920,8 @@ fphe_status fphe_neg(fphe_ctx* c, const uint32_t* Ca, size_t count, uint32_t* Co
   }
   const size_t xbytes = (size_t)ntiles_of(count) * c->L1 * FPHE_WAVE * 4;
   if (ensure_scratch(c, xbytes, (hipStream_t)stream) != FPHE_OK) return FPHE_ERR_HIP;
-  if (c->L2 == 128) launch_inv27<128>(c, Ca, count, nullptr, Co, err, c->scratch, (hipStream_t)stream);
+  if (c->L2 == 256) launch_inv27<256>(c, Ca, count, nullptr, Co, err, c->scratch, (hipStream_t)stream);
+  else if (c->L2 == 128) launch_inv27<128>(c, Ca, count, nullptr, Co, err, c->scratch, (hipStream_t)stream);
   else launch_inv27<64>(c, Ca, count, nullptr, Co, err, c->scratch, (hipStream_t)stream);
   return hip_ok(hipGetLastError());
 }
@@ -1875,6 +1934,7 @@ fphe_status fphe_sqmul(fphe_ctx* c, const uint32_t* Ca, const uint32_t* Cb, cons
   if (!Ca || !Cb || !sb || !Co || !so || nsq > (1u << 20)) return FPHE_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DevGuard g(c->device);
+  if (c->L2 == 256) return launch_sqmul27<256>(c, Ca, Cb, sb, (int)nsq, count, Co, so, (hipStream_t)stream);
   if (c->L2 == 128) return launch_sqmul27<128>(c, Ca, Cb, sb, (int)nsq, count, Co, so, (hipStream_t)stream);
   return launch_sqmul27<64>(c, Ca, Cb, sb, (int)nsq, count, Co, so, (hipStream_t)stream);
 }
@@ -1887,6 +1947,7 @@ fphe_status fphe_align(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, const
   if (!Ca || !sa || !gap || !Co || !so) return FPHE_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DevGuard g(c->device);
+  if (c->L2 == 256) return launch_align27<256>(c, Ca, sa, gap, count, Co, so, (hipStream_t)stream);
   if (c->L2 == 128) return launch_align27<128>(c, Ca, sa, gap, count, Co, so, (hipStream_t)stream);
   return launch_align27<64>(c, Ca, sa, gap, count, Co, so, (hipStream_t)stream);
 }
@@ -1900,6 +1961,8 @@ fphe_status fphe_mul(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, const i
   if (!Ca || !sa || !ea || !P || !pneg || !pexp || !Co || !so || !eo || lp == 0) return FPHE_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DevGuard g(c->device);
+  if (c->L2 == 256)
+    return launch_mul27<256>(c, Ca, sa, ea, P, lp, pneg, pexp, p_stride, count, Co, so, eo, err, (hipStream_t)stream);
   if (c->L2 == 128)
     return launch_mul27<128>(c, Ca, sa, ea, P, lp, pneg, pexp, p_stride, count, Co, so, eo, err, (hipStream_t)stream);
   return launch_mul27<64>(c, Ca, sa, ea, P, lp, pneg, pexp, p_stride, count, Co, so, eo, err, (hipStream_t)stream);

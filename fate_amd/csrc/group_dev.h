@@ -490,3 +490,94 @@ __global__ __launch_bounds__(kGrBlock) void k_gr_final(const u32* __restrict__ r
     }
   }
 }
+
+// --- ct-add launch order (fphe_add_order) ---------------------------------------------------------
+// The permutation k_add27 reads its slots through (paillier._add_order describes the why):
+// the slots are cut into kAoRuns runs of whole wave tiles (one per XCD, kAddRegions), a run
+// holds exactly the elements of its own element range, and inside a run
+//   1. the elements whose exponent gap is >= kAoHeavy, largest gap first (a gap-31 tile is
+//      ~25 ordinary tiles long: it must start early), then
+//   2. block by block (kAoBlock elements), the rest by gap, largest first.
+// A counting sort on (run, block, gap bin): per-block bin counts in LDS, one scan per run, an
+// LDS-atomic scatter per block.  The order of equal-bin elements inside a block is whatever
+// the atomics give: any order is a valid launch order (every slot computes its own element),
+// so the ct-add results are the same bits.
+constexpr int kAoRuns = 8;
+constexpr int kAoBlock = 4096;
+constexpr int kAoHeavy = 3;
+constexpr int kAoBins = 64;  // bin = 63 - min(gap, 63): heavy bins [0, 61), light bins 61..63
+
+__device__ __forceinline__ int ao_bin(const int32_t* __restrict__ ea, const int32_t* __restrict__ eb, size_t e) {
+  const long long d = (long long)ea[e] - eb[e];
+  const long long a = d < 0 ? -d : d;
+  return 63 - (int)(a > 63 ? 63 : a);
+}
+
+// counts[(blk * kAoBins + bin)], blk = global block index (run-major: run r's blocks are
+// [r * nbr, r * nbr + nbr)); one workgroup per block
+__global__ __launch_bounds__(kGrBlock) void k_ao_count(const int32_t* __restrict__ ea, const int32_t* __restrict__ eb,
+                                                       size_t m, size_t run, u32 nbr, int32_t* __restrict__ counts) {
+  __shared__ int32_t c[kAoBins];
+  const u32 blk = blockIdx.x, r = blk / nbr, b = blk % nbr;
+  if (threadIdx.x < kAoBins) c[threadIdx.x] = 0;
+  __syncthreads();
+  const size_t e0 = (size_t)r * run + (size_t)b * kAoBlock;
+  const size_t rend = (size_t)(r + 1) * run < m ? (size_t)(r + 1) * run : m;
+  const size_t e1 = e0 + kAoBlock < rend ? e0 + kAoBlock : rend;
+  for (size_t e = e0 + threadIdx.x; e < e1; e += kGrBlock) atomicAdd(&c[ao_bin(ea, eb, e)], 1);
+  __syncthreads();
+  if (threadIdx.x < kAoBins) counts[(size_t)blk * kAoBins + threadIdx.x] = c[threadIdx.x];
+}
+
+// one workgroup per run: offsets[(blk * kAoBins + bin)] = the slot of the block's first
+// element of that bin.  Scan order: the heavy bins bin-major across the run's blocks, then the
+// light bins block-major; each thread scans a contiguous piece of that sequence, then the
+// pieces' totals are scanned in LDS.
+__device__ __forceinline__ size_t ao_seq(size_t i, u32 nbr) {  // sequence position -> counter index
+  const size_t nh = (size_t)(kAoBins - kAoHeavy) * nbr;
+  if (i < nh) return (i % nbr) * kAoBins + i / nbr;
+  const size_t j = i - nh;
+  return (j / kAoHeavy) * kAoBins + (kAoBins - kAoHeavy) + j % kAoHeavy;
+}
+
+__global__ __launch_bounds__(kGrBlock) void k_ao_scan(const int32_t* __restrict__ counts, size_t run, u32 nbr,
+                                                       int32_t* __restrict__ offsets) {
+  __shared__ int32_t part[kGrBlock];
+  const u32 r = blockIdx.x;
+  const int32_t* c = counts + (size_t)r * nbr * kAoBins;
+  int32_t* o = offsets + (size_t)r * nbr * kAoBins;
+  const size_t total = (size_t)nbr * kAoBins, per = (total + kGrBlock - 1) / kGrBlock;
+  const size_t i0 = threadIdx.x * per, i1 = i0 + per < total ? i0 + per : total;
+  int32_t sum = 0;
+  for (size_t i = i0; i < i1; ++i) sum += c[ao_seq(i, nbr)];
+  part[threadIdx.x] = sum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int32_t acc = (int32_t)((size_t)r * run);
+    for (int t = 0; t < kGrBlock; ++t) {
+      const int32_t v = part[t];
+      part[t] = acc;
+      acc += v;
+    }
+  }
+  __syncthreads();
+  int32_t pos = part[threadIdx.x];
+  for (size_t i = i0; i < i1; ++i) {
+    const size_t k = ao_seq(i, nbr);
+    o[k] = pos;
+    pos += c[k];
+  }
+}
+
+__global__ __launch_bounds__(kGrBlock) void k_ao_scatter(const int32_t* __restrict__ ea, const int32_t* __restrict__ eb,
+                                                         size_t m, size_t run, u32 nbr,
+                                                         const int32_t* __restrict__ offsets, int32_t* __restrict__ ord) {
+  __shared__ int32_t o[kAoBins];
+  const u32 blk = blockIdx.x, r = blk / nbr, b = blk % nbr;
+  if (threadIdx.x < kAoBins) o[threadIdx.x] = offsets[(size_t)blk * kAoBins + threadIdx.x];
+  __syncthreads();
+  const size_t e0 = (size_t)r * run + (size_t)b * kAoBlock;
+  const size_t rend = (size_t)(r + 1) * run < m ? (size_t)(r + 1) * run : m;
+  const size_t e1 = e0 + kAoBlock < rend ? e0 + kAoBlock : rend;
+  for (size_t e = e0 + threadIdx.x; e < e1; e += kGrBlock) ord[atomicAdd(&o[ao_bin(ea, eb, e)], 1)] = (int32_t)e;
+}

@@ -161,7 +161,7 @@ def _pad_flat(x: torch.Tensor, n: int) -> torch.Tensor:
 # --------------------------------------------------------------------------------------
 # per-device key contexts
 # --------------------------------------------------------------------------------------
-MIN_KEY_BITS, MAX_KEY_BITS = 256, 2048
+MIN_KEY_BITS, MAX_KEY_BITS = 256, 4096
 
 
 def supports(key_bits: int) -> bool:
@@ -180,8 +180,8 @@ class _KeyCtx:
         if not supports(self.key_bits):
             raise ValueError(f"unsupported key size {self.key_bits}: this backend runs even sizes "
                              f"{MIN_KEY_BITS}..{MAX_KEY_BITS} (larger keys stay on the CPU fate_utils path)")
-        # geometry: the 1024- or 2048-bit kernels, n zero-padded up to it
-        self.L1 = 32 if self.key_bits <= 1024 else 64
+        # geometry: the 1024-, 2048- or 4096-bit kernels, n zero-padded up to it
+        self.L1 = 32 if self.key_bits <= 1024 else (64 if self.key_bits <= 2048 else 128)
         self.L2 = 2 * self.L1
         self._ctx: Dict[int, ctypes.c_void_p] = {}
         self._lock = threading.Lock()
@@ -792,8 +792,11 @@ class CiphertextVector:
         if ii.numel() == 0:
             return
         dev = self.device
-        ii, pp = ii.to(dev, torch.int64), pp.to(dev, torch.int64)
-        t = torch.arange(stride, device=dev)
+        # int32 index arithmetic when every source row and slot fits (fphe_fold_segments takes
+        # int32 indexes): half the bytes of the int64 expansion on 8M-term histograms
+        it = torch.int32 if max(other.count, self.count) * max(stride, 1) < (1 << 31) else torch.int64
+        ii, pp = ii.to(dev, it), pp.to(dev, it)
+        t = torch.arange(stride, device=dev, dtype=it)
         src = (ii[:, None] * stride + t).reshape(-1)
         slot = (pp[:, None] * stride + t).reshape(-1)
         # one ciphertext per slot (the literal 1 where no term lands: add's identity), then
@@ -947,13 +950,27 @@ def _add_order(ea: torch.Tensor, eb: torch.Tensor, L2: int) -> Optional[torch.Te
     With float data the gaps differ from element to element, so most waves pay for an
     outlier; sorted by gap, a wave's elements need the same number of squarings.  The kernel
     reads and writes the elements in place through the order (no gather or scatter
-    copies), and the order is a stable one-byte-key sort on the device (largest gaps first,
-    so the few long waves start at the head of the grid; gaps past 63 share the first
-    bucket): no host synchronisation, ~0.1 ms per 1M elements.  Returns the int32
-    permutation."""
-    d = (ea.to(torch.int32) - eb.to(torch.int32)).abs()
-    key = (63 - d.clamp(max=63)).to(torch.uint8)
-    return torch.sort(key, stable=True)[1].to(torch.int32)
+    copies).  k_add27 cuts the slots into ADD_REGIONS equal runs of wave tiles, one per XCD,
+    and the order keeps each run's elements in it: first the few with gaps >= 3, largest
+    first (a gap-31 tile is ~25 ordinary tiles long and must start early), then block by
+    block (4096 elements) the rest by gap.  The slots an XCD works on at once therefore map to
+    neighbouring elements, whose operand words share 128-byte lines in that XCD's L2 (HBM
+    traffic 5.8 -> 3.9 KB per element).  fphe_add_order builds it with a device counting sort:
+    no host synchronisation.  FPHE_ADD_REGION_SORT=0 selects round 2's global stable sort by
+    gap (A/B).  Returns the int32 permutation."""
+    if not _ADD_REGION_SORT:
+        d = (ea.to(torch.int32) - eb.to(torch.int32)).abs().clamp(max=63)
+        return torch.sort((63 - d).to(torch.uint8), stable=True)[1].to(torch.int32)
+    # the device counting sort of fphe_add_order (three small launches, ~0.05 ms per 1M):
+    # runs of whole wave tiles per XCD, gaps >= 3 at the head of each run (largest first),
+    # then the rest by gap within blocks of 4096 elements
+    m = ea.numel()
+    ea32 = ea.to(torch.int32).contiguous()
+    eb32 = eb.to(torch.int32).contiguous()
+    order = torch.empty(m, dtype=torch.int32, device=ea.device)
+    _lib.check(_lib.load().fphe_add_order(_ptr(ea32), _ptr(eb32), m, L2, _ptr(order),
+                                          ctypes.c_void_p(_stream(ea.device))), "fphe_add_order")
+    return order
 
 
 def _add(pk: "PK", a: CiphertextVector, b: CiphertextVector, broadcast: bool, count: Optional[int] = None,
@@ -1005,6 +1022,9 @@ def _flatten_positions(indexes, dev=None) -> Tuple[torch.Tensor, torch.Tensor]:
     return ii.to(dev, torch.int32), pp.to(dev, torch.int32)
 
 
+ADD_REGIONS = 8  # kAddRegions in fate_phe.hip: runs of k_add27 wave tiles, one per XCD
+# FPHE_ADD_REGION_SORT=0: one global gap sort (round-2 order; same-box A/B in tools/)
+_ADD_REGION_SORT = os.environ.get("FPHE_ADD_REGION_SORT", "1") != "0"
 FOLD_MAX = 64  # terms per chunk of fphe_fold (kFoldMax in kernels27.h)
 FOLD_TARGET_CHUNKS = 32768
 

@@ -159,7 +159,7 @@ class Coder:
 
 
 def supports(key_size: int) -> bool:
-    """Whether this backend runs keys of ``key_size`` bits (even, 256..2048).  The
+    """Whether this backend runs keys of ``key_size`` bits (even, 256..4096).  The
     ``PHECipherBuilder.setup`` branch in INTEGRATION.md keeps FATE's CPU module for the rest
     (the reference accepts any even size, paillier/src/lib.rs:72-87)."""
     return _p.supports(key_size)

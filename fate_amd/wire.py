@@ -197,9 +197,9 @@ def ciphertext_vector_to_bincode(cv: CiphertextVector, pk: Optional[PK] = None) 
     return bytes(res)
 
 
-# magnitude widths (32-bit words) of the kernels' two geometries: n^2 of <= 1024- and
-# <= 2048-bit keys; a key-less (raw) vector is read at the smaller one that holds its values
-RAW_WIDTHS = (64, 128)
+# magnitude widths (32-bit words) of the kernels' geometries: n^2 of <= 1024-, <= 2048- and
+# <= 4096-bit keys; a key-less (raw) vector is read at the smallest one that holds its values
+RAW_WIDTHS = (64, 128, 256)
 
 
 def _digit_bits(dig_len: np.ndarray, radix: np.ndarray) -> int:

@@ -17,7 +17,8 @@
  *    exp) are flat [T*64].  Buffers are padded to whole tiles.
  *  - A ciphertext vector is (C, sign, exp):
  *      C    : uint32 [T][L2][64]   canonical residue in [0, n^2), L2 = 64 for keys of at
- *                                  most 1024 bits, 128 up to 2048 (fphe_ctx_limbs)
+ *                                  most 1024 bits, 128 up to 2048, 256 up to 4096
+ *                                  (fphe_ctx_limbs)
  *      sign : uint8  [T*64]        1 iff the reference's signed integer is C - n^2
  *      exp  : int32  [T*64]        base-16 fixed-point exponent
  *    The reference keeps ciphertexts as signed rug::Integer values because rug's
@@ -65,9 +66,10 @@ typedef struct fphe_ctx fphe_ctx;
  * Replaces the key objects behind fate_utils.paillier.PK / SK
  * (paillier.rs:18-24; crates/paillier/src/lib.rs:49-69, SK::new :125-150).
  *   n      : L1 limbs (little-endian uint32, zero-padded), the public modulus, bits(n) ==
- *            key_bits (paillier/src/lib.rs:82); L1 = 32 for key_bits <= 1024, else 64.
+ *            key_bits (paillier/src/lib.rs:82); L1 = 32 for key_bits <= 1024, 64 up to
+ *            2048, else 128.
  *   p, q   : L1/2 limbs each (zero-padded), or both NULL for a public-only context.
- * key_bits: any even size 256..2048 (the reference takes any even size, lib.rs:72-87).
+ * key_bits: any even size 256..4096 (the reference takes any even size, lib.rs:72-87).
  * Keys below the geometry's width run its kernels with zero-padded limbs. */
 fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n,
                             const uint32_t* p, const uint32_t* q, fphe_ctx** out);
@@ -168,6 +170,18 @@ fphe_status fphe_add_ordered(fphe_ctx* ctx,
                              const uint32_t* Cb, const uint8_t* sb, const int32_t* eb, int b_stride,
                              size_t count, const int32_t* order, uint32_t* Co, uint8_t* so, int32_t* eo,
                              void* stream);
+
+/* Launch order for fphe_add_ordered over `count` element pairs (device arrays of the two
+ * operands' exponents): the permutation that groups the exponent gaps |ea - eb| (every
+ * element of a wave pays the wave's largest gap: 4 squarings per base-16 step, decrese_exp_to,
+ * fixedpoint_paillier/src/lib.rs:250-258).  The slots are cut into 8 runs of whole wave tiles
+ * (L2 = 64 / 128 / 256 sets the tile: 32 / 16 / 8 elements), one per XCD in fphe_add_ordered;
+ * run r holds exactly the elements of its own element range: first those with gaps >= 3,
+ * largest first, then block by block (4096 elements) the rest, largest gap first.  A device
+ * counting sort, no host synchronisation.  The order within a bin is not specified (any
+ * order gives the same ciphertexts).  order: int32 [count]. */
+fphe_status fphe_add_order(const int32_t* ea, const int32_t* eb, size_t count, uint32_t L2, int32_t* order,
+                           void* stream);
 
 /* Ciphertext x plaintext: CiphertextVector.mul (paillier.rs:361) -> Ciphertext::mul
  * (fixedpoint_paillier/src/lib.rs:334-349).  Plaintext (P[T][lp][64], neg, pexp);

@@ -146,6 +146,40 @@ def test_add_gap_sorted_matches_kernel_order(k1024):
     assert torch.allclose(d, x.double() + y.double(), rtol=1e-12, atol=0)
 
 
+@pytest.mark.parametrize("m,L2", [(1, 128), (4097, 128), (70000, 64), (300001, 128), (1 << 20, 256)])
+def test_add_order_device_counting_sort(m, L2):
+    """fphe_add_order (the ct-add launch order) against its contract: a permutation; run r
+    (ceil(wave tiles / 8) tiles) holds exactly its own element range; inside a run the gaps
+    >= 3 come first in non-increasing order, then every 4096-element block's elements
+    contiguously, non-increasing gaps within the block."""
+    g = torch.Generator().manual_seed(m)
+    eb = torch.randint(-40, 40, (m,), generator=g, dtype=torch.int32)
+    d = torch.multinomial(torch.tensor([0.37, 0.55, 0.05, 0.02, 0.01]), m, replacement=True, generator=g)
+    d = d.to(torch.int32) * torch.where(torch.rand(m, generator=g) < 0.001, 20, 1).to(torch.int32)
+    ea = eb + d * torch.where(torch.rand(m, generator=g) < 0.5, 1, -1).to(torch.int32)
+    o = P._add_order(ea.cuda(), eb.cuda(), L2).cpu().long()
+    assert torch.equal(torch.sort(o)[0], torch.arange(m))
+    E = 64 // (L2 // 32)
+    nwt = (m + E - 1) // E
+    run = (nwt + 7) // 8 * E
+    gap = (ea - eb).abs().clamp(max=63)
+    for r in range(8):
+        lo, hi = r * run, min((r + 1) * run, m)
+        if lo >= hi:
+            continue
+        seg = o[lo:hi]
+        assert int(seg.min()) >= lo and int(seg.max()) < hi
+        gs = gap[seg]
+        nh = int((gs >= 3).sum())
+        assert bool((gs[:nh] >= 3).all()) and bool((gs[nh:] < 3).all())
+        assert bool((gs[:nh][1:] <= gs[:nh][:-1]).all())
+        light, lg = seg[nh:], gs[nh:]
+        blk = (light - lo) // 4096
+        assert bool((blk[1:] >= blk[:-1]).all())  # blocks in order, each contiguous
+        same = blk[1:] == blk[:-1]
+        assert bool((lg[1:][same] <= lg[:-1][same]).all())
+
+
 @pytest.mark.parametrize("bits", [1024, 2048])
 def test_export_import_signed(bits):
     """fphe_export_signed / fphe_import_signed against the host conversion of the fixtures'
@@ -246,19 +280,22 @@ def test_random_op_chains_vs_oracle(bits, seed):
     assert [float(x) for x in got] == [float(x) for x in want]
 
 
-@pytest.mark.parametrize("bits", [256, 258, 512, 770, 1026, 1030, 1536])
+@pytest.mark.parametrize("bits", [256, 258, 512, 770, 1026, 1030, 1536, 2050, 3072, 4096])
 def test_other_key_sizes_bit_exact(bits):
     """Even key sizes other than 1024 / 2048 (the reference takes any even size, paillier/
-    src/lib.rs:72-87; he_param.key_length is a job parameter) run the 1024- or 2048-bit
-    kernels with n zero-padded: encrypt (public and key-holder, injected r), ct-add with
-    exponent alignment, ct x pt with negative weights, neg and decrypt, bit-exact against
-    the oracle on a freshly generated key."""
+    src/lib.rs:72-87; he_param.key_length is a job parameter) run the 1024-, 2048- or 4096-bit
+    kernels with n zero-padded (above 2048 bits n^2 spans 8 lanes per element, TPI 8):
+    encrypt (public and key-holder, injected r), ct-add with exponent alignment, ct x pt with
+    negative weights, neg and decrypt, bit-exact against the oracle on a freshly generated
+    key, and the public-key encryptions against libgmp."""
     import random
+    from oracle import gmp_ref
     sk, pk, coder = P.keygen(bits)
     assert pk.n.bit_length() == bits
     osk, opk = O.keypair_from_primes(sk.p, sk.q)
     rng = random.Random(bits)
-    xs = [rng.uniform(-9, 9) for _ in range(70)] + [0.0, -1e-300, 3e38]
+    nx = 70 if bits <= 2048 else 40  # the Python oracle's powm at 8192 bits is the slow side
+    xs = [rng.uniform(-9, 9) for _ in range(nx)] + [0.0, -1e-300, 3e38]
     ws = [rng.uniform(-2, 2) for _ in xs]
     rs = [1 + rng.randrange(pk.n - 1) for _ in xs]
     xd = torch.tensor(xs, dtype=torch.float64, device="cuda")
@@ -269,6 +306,9 @@ def test_other_key_sizes_bit_exact(bits):
     oc = [O.fp_encrypt(opk, O.encode_f64(opk.n, x), True, r) for x, r in zip(xs, rs)]
     want = ([o.c for o in oc], [o.exp for o in oc])
     assert c.to_signed_ints(pk.ns) == want and ck.to_signed_ints(pk.ns) == want
+    gk = gmp_ref.GmpKey(pk.n, sk.p, sk.q)
+    sig, _ = pv.to_ints()
+    assert want[0] == [gk.encrypt(s_, r, True) for s_, r in zip(sig, rs)]
     y = pub.encrypt_encoded(coder.encode_f64_vec(xd.flip(0) * 1e-3), True, r=rs[::-1])
     oy = [O.fp_encrypt(opk, O.encode_f64(opk.n, x * 1e-3), True, r) for x, r in zip(xs[::-1], rs[::-1])]
     s = c.add(pk, y)
@@ -287,9 +327,10 @@ def test_unsupported_key_sizes_decline():
     """Sizes this backend does not run fail at keygen with ValueError (FATE keeps its CPU
     path for them); odd sizes fail like the reference's assert."""
     from fate_amd import protocol as PR
-    assert PR.supports(2048) and PR.supports(1536) and not PR.supports(3072) and not PR.supports(1023)
+    assert PR.supports(2048) and PR.supports(1536) and PR.supports(3072) and PR.supports(4096)
+    assert not PR.supports(4098) and not PR.supports(1023) and not PR.supports(254)
     with pytest.raises(ValueError):
-        PR.keygen(3072)
+        PR.keygen(4098)
     with pytest.raises(AssertionError):
         P.keygen(1023)
 

@@ -140,17 +140,18 @@ def test_chacha20_symbol_exported():
 
 
 def test_key_size_gate():
-    """Even sizes 256..2048 run on the device geometry; others decline at keygen (ValueError)
-    before any prime is drawn; odd sizes fail like the reference's assert
-    (paillier/src/lib.rs:73)."""
+    """Even sizes 256..4096 run on the device geometries (1024-, 2048-, 4096-bit); others
+    decline at keygen (ValueError) before any prime is drawn; odd sizes fail like the
+    reference's assert (paillier/src/lib.rs:73)."""
     import pytest
     from fate_amd import paillier as P
     from fate_amd import protocol as PR
-    assert all(PR.supports(b) for b in (256, 512, 1024, 1030, 1536, 2048))
-    assert not any(PR.supports(b) for b in (254, 1023, 2050, 3072, 4096))
+    assert all(PR.supports(b) for b in (256, 512, 1024, 1030, 1536, 2048, 2050, 3072, 4096))
+    assert not any(PR.supports(b) for b in (254, 1023, 4098, 8192))
     with pytest.raises(ValueError):
-        PR.keygen(4096)
+        PR.keygen(4098)
     with pytest.raises(AssertionError):
         P.keygen(1023)
     pk = P.PK(P.keygen(512)[1].n)
     assert pk._key.L1 == 32 and pk._key.L2 == 64
+    assert P.PK((1 << 3071) + 1)._key.L2 == 256

@@ -64,11 +64,11 @@ def test_generated_asm_headers_in_sync():
                                os.path.join(ROOT, "fate_amd", "csrc", name), shallow=False), name
 
 
-@pytest.mark.parametrize("tpi,ll", [(4, 38), (2, 38), (1, 38), (2, 37), (1, 37)])
+@pytest.mark.parametrize("tpi,ll", [(4, 38), (2, 38), (1, 38), (8, 37), (4, 37), (2, 37), (1, 37)])
 def test_squaring_window_adds_every_limb_pair_once(tpi, ll):
     """The half-product squaring (mont_engine.inc mont_sqr, rows from the generator's
     sq_window) adds each off-diagonal limb pair exactly twice (once, doubled) and each
-    diagonal term once, for the 27 x 38 (TPI 4) and 28 x 37 (TPI 1, 2) engines.  Multiplier
+    diagonal term once, for the 27 x 38 (TPI 4) and 28 x 37 (TPI 1, 2, 4, 8) engines.  Multiplier
     rules as the kernel's bit-field masks: bf = 2a (q > s), a (q == s), 0 (q < s); bl (even
     LL only) = 2a if q < s or (q == s and a < LL/2), else 0; bm = 2a."""
     import importlib.util

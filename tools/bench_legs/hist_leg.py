@@ -28,6 +28,8 @@ if len(sys.argv) > 3 and sys.argv[3] == "mul":
     print(json.dumps({"distinct_exps": int(torch.unique(gh.exp[: 2 * N]).numel())}), flush=True)
 bins = torch.randint(0, NB, (N, HF), generator=g)
 positions = bins + torch.arange(HF) * NB
+if os.environ.get("HIST_HOST_POSITIONS") != "1":
+    positions = positions.to(dev, torch.int32)  # device-resident bin indexes (bench.py)
 T = {}
 orig = {name: getattr(P, name) for name in ("_fold_to_segments", "_fold_segments", "_fold_chunks", "_fold_tree", "_add", "_add_order")}
 

@@ -71,7 +71,11 @@ def gen(LL, LB):
     def treg(k):
         return "v[2:3]" if k == 0 else ("v[4:5]" if k == LL - 1 else f"%[t{k}]")
 
-    def fused(pos, spread, carry64=True):
+    def fused(pos, spread, carry64=True, half_row=False):
+        # half_row (TPI 8): the element spans 8 lanes, so m's broadcast takes a second DPP
+        # step -- the upper quad of each half row (banks 1, 3) copies the lower quad's value
+        # by row_half_mirror -- at least two VALU instructions after the first (DPP read of a
+        # VALU-written VGPR), still ahead of the reduction MACs that read m
         m_gap, x_gap, c_gap = spread
         opm = [f"v_mad_u64_u32 {treg(k)}, vcc, %[a{k}], %[{mul}], {treg(k)}" for k, mul in pos]
         seq = []
@@ -83,7 +87,14 @@ def gen(LL, LB):
         if len(lead) < 2:
             seq.append("s_nop 1")
         seq.append("@BC@")
-        seq += opm[m_gap:]
+        rest = opm[m_gap:]
+        if half_row:
+            seq += rest[:2]
+            if len(rest) < 2:
+                seq.append("s_nop 1")
+            seq.append("v_mov_b32_dpp v11, v11 row_half_mirror row_mask:0xf bank_mask:0xa")
+            rest = rest[2:]
+        seq += rest
         redm = [f"v_mad_u64_u32 {treg(j - 1)}, vcc, v11, %[n{j}], {treg(j)}" for j in range(1, LL)]
         seq.append("v_mad_u64_u32 v[6:7], vcc, v11, %[n0], v[2:3]")
         seq += redm[:x_gap]
@@ -117,10 +128,11 @@ def gen(LL, LB):
     spread_macros = {}
     for sp, spread in SPREADS.items():
         lst = []
-        for fam, c64 in (("RGF", True), ("RGF2", False)):  # RGF: TPI 4 rows, RGF2: TPI 2 rows
-            lst.append((f"{fam}_ROW(BC)", fused([(k, "b") for k in range(LL)], spread, c64)))
+        # RGF: TPI 4 rows, RGF2: TPI 2 rows, RGF8: TPI 8 rows (keys above 2048 bits)
+        for fam, c64, hr in (("RGF", True, False), ("RGF2", False, False), ("RGF8", True, True)):
+            lst.append((f"{fam}_ROW(BC)", fused([(k, "b") for k in range(LL)], spread, c64, hr)))
             for a in range(LL):
-                lst.append((f"{fam}_SQROW_{a}(BC)", fused(window(a), spread, c64)))
+                lst.append((f"{fam}_SQROW_{a}(BC)", fused(window(a), spread, c64, hr)))
         spread_macros[sp] = lst
 
     out = [f"// Generated by tools/gen_mont27_asm.py -- do not edit.  {LL} limbs of {LB} bits per lane.",
@@ -146,7 +158,7 @@ def gen(LL, LB):
         out.append("}")
     out.append("#elif RG_SECTION == 3")
     out.append("template <int TPI, int a> __device__ __forceinline__ void r27f_sqrow(u64 (&T)[LL], const L27& A, u32 bf, u32 bm, u32 bl, const Mod<TPI>& N, u32 np, u32 mk);")
-    tpis = ((4, "quad_perm:[0,0,0,0]", "RGF"), (2, "quad_perm:[0,0,2,2]", "RGF2"))
+    tpis = ((4, "quad_perm:[0,0,0,0]", "RGF"), (2, "quad_perm:[0,0,2,2]", "RGF2"), (8, "quad_perm:[0,0,0,0]", "RGF8"))
     for a in range(LL):
         for tpi, bc, fam in tpis:
             out.append(f"template <> __device__ __forceinline__ void r27f_sqrow<{tpi}, {a}>(u64 (&T)[LL], const L27& A, u32 bf, u32 bm, u32 bl, const Mod<{tpi}>& N, u32 np, u32 mk) {{")
