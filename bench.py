@@ -657,6 +657,35 @@ def main() -> None:
                  "encrypt_roofline_frac": round(N * enc_mac32_per_elem(1024) / (enc1_ms / 1e3) / 1e12 / PEAK_TMAC32, 4),
                  "decrypt_roofline_frac": round(N * dec_mac32_per_elem(1024) / (dec1_ms / 1e3) / 1e12 / PEAK_TMAC32, 4)}
         del c1, d1, y1, pv1
+        # 4096-bit keys (the TPI-8 geometry; he_param.key_length is a job parameter): rates on
+        # the first 2^16 elements (a 4096-bit encrypt is ~8x a 2048-bit one), round trip
+        k4096 = None
+        kpath = os.path.join(ROOT, "tests", "golden", "key_4096.json")
+        if os.path.exists(kpath):
+            with open(kpath) as f:
+                fx4 = json.load(f)
+            sk4, pk4, coder4 = P.keypair_from_primes(int(fx4["p"], 16), int(fx4["q"], 16), keyholder=False)
+            n4 = min(N, 1 << 16)
+            pv4 = coder4.encode_f32_vec(xd[:n4])
+            sk4.decrypt_to_encoded(pk4.encrypt_encoded(pv4, True))  # untimed: scratch growth
+            torch.cuda.synchronize(dev)
+            e0.record(stream)
+            c4 = pk4.encrypt_encoded(pv4, True)
+            e1.record(stream)
+            torch.cuda.synchronize(dev)
+            enc4_ms = e0.elapsed_time(e1)
+            e0.record(stream)
+            d4 = sk4.decrypt_to_encoded(c4)
+            e1.record(stream)
+            torch.cuda.synchronize(dev)
+            dec4_ms = e0.elapsed_time(e1)
+            y4 = coder4.decode_f32_vec(d4)
+            k4096 = {"elements": n4, "encrypt_per_s": round(n4 / (enc4_ms / 1e3), 1),
+                     "decrypt_per_s": round(n4 / (dec4_ms / 1e3), 1),
+                     "roundtrip_bit_exact": bool(np.array_equal(y4.cpu().numpy().view(np.uint32), xb[:n4])),
+                     "encrypt_roofline_frac": round(n4 * enc_mac32_per_elem(4096) / (enc4_ms / 1e3) / 1e12 / PEAK_TMAC32, 4),
+                     "decrypt_roofline_frac": round(n4 * dec_mac32_per_elem(4096) / (dec4_ms / 1e3) / 1e12 / PEAK_TMAC32, 4)}
+            del c4, d4, y4, pv4
         # key-holder encryption (CRT halves): throughput, round trip, and identity with the
         # public-key path on a subset with the same injected r
         torch.cuda.synchronize(dev)
@@ -691,6 +720,7 @@ def main() -> None:
             "histogram_multi_gpu": hist_mgpu,
             "hetero_lr_gradient": hlr,
             "key_1024": k1024,
+            "key_4096": k4096,
             "decrypt_per_s": round(N / (dec_ms / 1e3), 1),
             "ct_add_per_s": round(N / (add_ms / 1e3), 1),
             "e2e_host_encrypts_per_s": round(N / e2e, 1),

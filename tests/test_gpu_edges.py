@@ -528,3 +528,48 @@ def test_config2_subset_4096_vs_gmp():
     xb = x.view(torch.int32).clone()
     xb[xb == -2147483648] = 0  # -0.0
     assert torch.equal(bits, xb)
+
+
+@pytest.mark.parametrize("bits", [3072])
+def test_large_key_vector_ops_and_pickle(bits):
+    """The 4096-bit geometry (TPI 8) through the vector ops above the element-wise kernels:
+    the device-grouped fold under iupdate (terms with several exponents, negative signed
+    ciphertexts, literal 1s), cumsum, and the reference's pickle state (bincode of the signed
+    integers, paillier.rs:219-226) of an L2 = 256 vector, against the oracle's sequential
+    Ciphertext::add (fixedpoint_paillier/src/lib.rs:301-333, 724-771)."""
+    import pickle
+    import random
+    from fate_amd import wire
+    sk, pk, coder = P.keygen(bits)
+    osk, opk = O.keypair_from_primes(sk.p, sk.q)
+    assert pk._key.L2 == 256
+    rng = random.Random(bits + 1)
+    src = []
+    for i in range(150):
+        r = rng.random()
+        if r < 0.05:
+            src.append(O.Ciphertext(1, rng.choice([0, -14])))
+        else:
+            c = rng.randrange(2, opk.ns)
+            src.append(O.Ciphertext(-c if rng.random() < 0.3 else c, rng.choice([-14, -13, -13, -12, -15])))
+    dv = P.CiphertextVector.from_signed_ints([c.c for c in src], [c.exp for c in src], pk.ns, pk._key.L2)
+    # iupdate: 75 samples x (2 positions) x stride 2 into 10 x 2 slots
+    nslot = 10
+    positions = [[rng.randrange(nslot), rng.randrange(nslot)] for _ in range(75)]
+    hist = P.CiphertextVector.zeros(nslot * 2, pk._key.L2)
+    hist.iupdate(dv, positions, 2, pk)
+    want = [O.ct_zero() for _ in range(nslot * 2)]
+    O.iupdate(opk, want, src, positions, 2)
+    assert hist.to_signed_ints(pk.ns) == ([c.c for c in want], [c.exp for c in want])
+    # cumsum with step 1 over two chunks
+    cv = P.CiphertextVector.from_signed_ints([c.c for c in src[:40]], [c.exp for c in src[:40]], pk.ns, pk._key.L2)
+    cv.chunking_cumsum_with_step(pk, [25, 15], 1)
+    ref = list(src[:40])
+    O.chunking_cumsum_with_step(opk, ref, [25, 15], 1)
+    assert cv.to_signed_ints(pk.ns) == ([c.c for c in ref], [c.exp for c in ref])
+    # the reference's pickle state at L2 = 256, and back
+    state = wire.ciphertext_vector_to_bincode(dv, pk)
+    back, used = wire.ciphertext_vector_from_bincode(state, pk)
+    assert used == len(state) and back.to_signed_ints(pk.ns) == dv.to_signed_ints(pk.ns)
+    raw = pickle.loads(pickle.dumps(dv))
+    assert raw.to_signed_ints() == ([c.c for c in src], [c.exp for c in src])

@@ -31,7 +31,8 @@ positions = bins + torch.arange(HF) * NB
 if os.environ.get("HIST_HOST_POSITIONS") != "1":
     positions = positions.to(dev, torch.int32)  # device-resident bin indexes (bench.py)
 T = {}
-orig = {name: getattr(P, name) for name in ("_fold_to_segments", "_fold_segments", "_fold_chunks", "_fold_tree", "_add", "_add_order")}
+orig = {name: getattr(P, name) for name in ("_fold_to_segments", "_fold_segments", "_fold_chunks", "_fold_tree", "_add",
+                                             "_add_order", "_flatten_positions", "_fit_limbs", "_fold_check")}
 
 
 def timed(name):
