@@ -1564,11 +1564,12 @@ fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, 
     c->cus = prop.multiProcessorCount;
     {
       // fphe_fold_segments takes its scratch from the device's default stream-ordered pool:
-      // keep up to 8 GiB of it cached across calls (the default threshold of 0 hands every
-      // block back to the driver at each synchronisation, and a 1-GiB re-map costs ms)
+      // keep up to 24 GiB of it cached across calls (the default threshold of 0 hands every
+      // block back to the driver at each synchronisation, and a 1-GiB re-map costs ms; a
+      // 200M-term histogram over 20M source ciphertexts uses ~12 GiB, of 288 GiB of HBM)
       hipMemPool_t pool;
       if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
-        uint64_t keep = (uint64_t)8 << 30;
+        uint64_t keep = (uint64_t)24 << 30;
         (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
       }
     }
