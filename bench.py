@@ -577,23 +577,40 @@ def main() -> None:
         # SecureBoost histogram (BASELINE config 4 shape at one GPU): (g, h) interleaved with
         # stride 2, HF features x 32 bins, iupdate = per-bin ct-add fold on the device
         HF, NB = 4, 32
-        gh = P.Evaluator.cat([ct, ct2])._gather(torch.stack([torch.arange(N), N + torch.arange(N)], 1).reshape(-1))
         gb = torch.Generator().manual_seed(99 + rank)
         bins = torch.randint(0, NB, (N, HF), generator=gb)
         positions = bins + torch.arange(HF) * NB
         # the bin indexes are input data, resident in HBM like the ciphertexts (the binning
         # step that makes them runs on the device too); the host-list rate is reported beside
         positions_d = positions.to(dev, torch.int32)
-        # untimed full-size pass first, as for the other legs: the call's stream-ordered
-        # scratch (term keys, element-major rows, partials: ~0.6 GB here) is mapped into the
-        # device pool there, not in the timed call
-        P.CiphertextVector.zeros(HF * NB * 2, pk._key.L2, dev).iupdate(gh, positions_d, 2, pk)
-        hist = P.CiphertextVector.zeros(HF * NB * 2, pk._key.L2, dev)
-        torch.cuda.synchronize(dev)
-        t0h = time.perf_counter()
-        hist.iupdate(gh, positions_d, 2, pk)
-        torch.cuda.synchronize(dev)
-        hist_s = time.perf_counter() - t0h
+        # SecureBoost-shaped gradients (as tools/bench_legs/secureboost_full.py): g = p - y,
+        # h = p (1 - p), encrypted by the guest (key holder, untimed), interleaved (g, h)
+        psig = torch.sigmoid(torch.randn(N, generator=gb, dtype=torch.float64))
+        ylab = (torch.rand(N, generator=gb, dtype=torch.float64) < 0.5).double()
+        g_sb, h_sb = (psig - ylab).float(), (psig * (1 - psig)).float()
+        gh = pk_kh.encrypt_encoded(coder.encode_f32_vec(torch.stack([g_sb, h_sb], 1).reshape(-1).to(dev)), True)
+
+        def run_hist(src, wg, wh):
+            # untimed full-size pass first, as for the other legs: the call's stream-ordered
+            # scratch (term keys, element-major rows, partials: ~0.6 GB here) is mapped into
+            # the device pool there, not in the timed call
+            P.CiphertextVector.zeros(HF * NB * 2, pk._key.L2, dev).iupdate(src, positions_d, 2, pk)
+            hh = P.CiphertextVector.zeros(HF * NB * 2, pk._key.L2, dev)
+            torch.cuda.synchronize(dev)
+            t0h = time.perf_counter()
+            hh.iupdate(src, positions_d, 2, pk)
+            torch.cuda.synchronize(dev)
+            secs = time.perf_counter() - t0h
+            # property check: decrypted bins == float64 sums of the encoded inputs
+            hd = coder.decode_f64_vec(sk.decrypt_to_encoded(hh)).cpu().reshape(HF * NB, 2)
+            want = torch.zeros(HF * NB, 2, dtype=torch.float64)
+            for f in range(HF):
+                want[:, 0].index_add_(0, positions[:, f], wg)
+                want[:, 1].index_add_(0, positions[:, f], wh)
+            fin = torch.isfinite(want)
+            return hh, secs, bool(torch.allclose(hd[fin], want[fin], rtol=1e-9, atol=1e-6)), want
+
+        hist, hist_s, hist_ok, want = run_hist(gh, g_sb.double(), h_sb.double())
         hist_h = P.CiphertextVector.zeros(HF * NB * 2, pk._key.L2, dev)
         torch.cuda.synchronize(dev)
         t0h = time.perf_counter()
@@ -602,16 +619,14 @@ def main() -> None:
         hist_host_s = time.perf_counter() - t0h
         del hist_h
         iupdate_block = iupdate_roofline(gh, positions, 2, HF * NB * 2, hist_s, key_bits)
-        # property check: decrypted bins == float64 sums of the encoded inputs
-        hd = coder.decode_f64_vec(sk.decrypt_to_encoded(hist)).cpu().reshape(HF * NB, 2)
-        xg = x.double()
-        xh = torch.flip(x, [0]).double() * 0.25
-        want = torch.zeros(HF * NB, 2, dtype=torch.float64)
-        for f in range(HF):
-            want[:, 0].index_add_(0, positions[:, f], xg)
-            want[:, 1].index_add_(0, positions[:, f], xh)
-        fin = torch.isfinite(want)
-        hist_ok = bool(torch.allclose(hd[fin], want[fin], rtol=1e-9, atol=1e-6))
+        # the same fold over the encrypt leg's vector and its mirror (x with the edge values
+        # 0, +-1e-30, +-3.4e38 among the first inputs): exponent gaps up to 31 force one
+        # 124-squaring alignment chain, a ~4.8 ms critical path on a single wave
+        gh_edge = P.Evaluator.cat([ct, ct2])._gather(torch.stack([torch.arange(N), N + torch.arange(N)], 1).reshape(-1))
+        he, hist_edge_s, hist_edge_ok, _ = run_hist(gh_edge, x.double(), torch.flip(x, [0]).double() * 0.25)
+        hist_edge = {"iupdate_s": round(hist_edge_s, 5), "allclose": hist_edge_ok,
+                     "roofline_frac": iupdate_roofline(gh_edge, positions, 2, HF * NB * 2, hist_edge_s, key_bits)["frac"]}
+        del he, gh_edge
         hist_mgpu = None
         if dist:
             # config 4 across GPUs: each rank folded its own samples; the
@@ -716,7 +731,9 @@ def main() -> None:
             "histogram_scatter_adds_per_s": round(N * HF * 2 / hist_s, 1),
             "histogram_iupdate_s": round(hist_s, 5),
             "histogram_iupdate_host_positions_s": round(hist_host_s, 5),
-            "histogram_config": f"{N} samples x {HF} features x {NB} bins x (g,h), iupdate fold on device",
+            "histogram_edge_values": hist_edge,
+            "histogram_config": f"{N} samples x {HF} features x {NB} bins x (g,h), SecureBoost-shaped g = p - y, "
+                                f"h = p(1 - p) (key-holder encryptions, untimed), iupdate fold on device",
             "histogram_allclose": hist_ok,
             "histogram_packed": packed,
             "histogram_multi_gpu": hist_mgpu,
