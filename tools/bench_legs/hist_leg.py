@@ -18,7 +18,10 @@ fx = json.load(open(os.path.join(ROOT, "tests", "golden", "paillier_2048.json"))
 sk, pk, coder = P.keypair_from_primes(int(fx["p"], 16), int(fx["q"], 16))
 dev = torch.device("cuda", 0)
 g = torch.Generator().manual_seed(1)
-x = (torch.randn(2 * N, generator=g) * 4).to(dev)
+# SecureBoost-shaped (g, h) pairs, interleaved (bench.py's histogram leg)
+psig = torch.sigmoid(torch.randn(N, generator=g, dtype=torch.float64))
+ylab = (torch.rand(N, generator=g, dtype=torch.float64) < 0.5).double()
+x = torch.stack([(psig - ylab).float(), (psig * (1 - psig)).float()], 1).reshape(-1).to(dev)
 gh = pk.encrypt_encoded(coder.encode_f32_vec(x), True)
 HF = int(sys.argv[2]) if len(sys.argv) > 2 else 4
 NB = 32
