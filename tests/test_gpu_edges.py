@@ -128,10 +128,15 @@ def test_permute_gather_assign_cat():
 
 
 
-def test_add_gap_sorted_matches_kernel_order(k1024):
-    """fphe_add over an exponent-gap-sorted order (fate_amd.paillier._add_order) gives the
-    same ciphertexts as the kernel in element order; decrypted sums match the floats."""
-    p, q, sk, pk, coder, osk, opk = k1024
+@pytest.mark.parametrize("bits", [1024, 3072])
+def test_add_gap_sorted_matches_kernel_order(k1024, bits):
+    """fphe_add over the device launch order (fate_amd.paillier._add_order: XCD runs, gap
+    bins) gives the same ciphertexts as the kernel in element order; decrypted sums match the
+    floats.  3072 bits: k_add27 on the TPI-8 geometry (8 elements per wave tile)."""
+    if bits == 1024:
+        p, q, sk, pk, coder, osk, opk = k1024
+    else:
+        sk, pk, coder = P.keygen(bits)
     n = 8192 + 33
     g = torch.Generator().manual_seed(9)
     x = torch.randn(n, generator=g) * torch.exp2(torch.randint(-12, 12, (n,), generator=g).float())
