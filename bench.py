@@ -121,31 +121,41 @@ def _profile_order(path: str):
     return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(path))]
 
 
+def _pmc_profile(kind: str, pattern: str):
+    """The committed PMC profile of this build: the one profiles/current_pmc.json names for
+    `kind`, else the newest matching file in natural order."""
+    import glob
+    cur = os.path.join(ROOT, "profiles", "current_pmc.json")
+    if os.path.exists(cur):
+        with open(cur) as f:
+            name = json.load(f).get(kind)
+        if name and os.path.exists(os.path.join(ROOT, name)):
+            return os.path.join(ROOT, name)
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "**", pattern), recursive=True), key=_profile_order)
+    return paths[-1] if paths else None
+
+
 def pmc_traffic_per_elem():
     """HBM bytes per element of k_encrypt27 from the committed rocprofv3 PMC passes
     (FETCH_SIZE and WRITE_SIZE in separate runs, FETCH_SIZE doubled per the calibration
     probe tools/probe/fetch_calib.hip), or None when no such profile is present."""
-    import glob
-    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "*pmc_encrypt27.json"), recursive=True),
-                   key=_profile_order)
-    if not paths:
+    path = _pmc_profile("encrypt27", "*pmc_encrypt27.json")
+    if not path:
         return None, None
-    with open(paths[-1]) as f:
+    with open(path) as f:
         d = json.load(f)
-    return float(d["hbm_bytes_per_elem"]), os.path.relpath(paths[-1], ROOT)
+    return float(d["hbm_bytes_per_elem"]), os.path.relpath(path, ROOT)
 
 
 def pmc_ops_traffic(op: str):
     """HBM bytes per element of the decrypt ("decrypt") or ct-add ("ct_add") kernels from the
     committed PMC passes (tools/pmc_ops_summary.py), or (None, None)."""
-    import glob
-    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "*pmc_ops.json"), recursive=True),
-                   key=_profile_order)
-    if not paths:
+    path = _pmc_profile("ops", "*pmc_ops.json")
+    if not path:
         return None, None
-    with open(paths[-1]) as f:
+    with open(path) as f:
         d = json.load(f)
-    return float(d[op]["hbm_bytes_per_elem"]), os.path.relpath(paths[-1], ROOT)
+    return float(d[op]["hbm_bytes_per_elem"]), os.path.relpath(path, ROOT)
 
 
 def _traffic(op: str, n: int):
