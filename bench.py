@@ -646,9 +646,10 @@ def main() -> None:
                 from fate_amd.dist import fold_across_ranks
                 barrier()
                 acc, t_gather, t_fold = fold_across_ranks(pk, hist)
-                wants = [torch.zeros_like(want) for _ in range(world)]
-                tdist.all_gather_object(wants, want)
-                want_all = sum(wants)
+                wd = want.to(dev)  # the float64 reference sums, gathered as device tensors like the shards
+                wants = [torch.empty_like(wd) for _ in range(world)]
+                tdist.all_gather(wants, wd)
+                want_all = sum(w.cpu() for w in wants)
                 got_all = coder.decode_f64_vec(sk.decrypt_to_encoded(acc)).cpu().reshape(HF * NB, 2)
                 fin_all = torch.isfinite(want_all)
                 hist_mgpu = {"ranks": world, "gather_s": round(t_gather, 4), "fold_s": round(t_fold, 4),
