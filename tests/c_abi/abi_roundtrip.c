@@ -57,13 +57,13 @@ int main(void) {
   size_t count = 0;
   static char buf[8192], rbuf[8192];
   if (scanf("%u", &bits) != 1) return 1;
-  uint32_t n[64], p[32], q[32];
+  uint32_t n[128], p[64], q[64]; /* keys up to 4096 bits (fphe_ctx_create reads L1 <= 128 words) */
   if (scanf("%8191s", buf) != 1) return 1;
-  parse_hex(buf, n, 64);
+  parse_hex(buf, n, 128);
   if (scanf("%8191s", buf) != 1) return 1;
-  parse_hex(buf, p, 32);
+  parse_hex(buf, p, 64);
   if (scanf("%8191s", buf) != 1) return 1;
-  parse_hex(buf, q, 32);
+  parse_hex(buf, q, 64);
   if (scanf("%zu", &count) != 1) return 1;
 
   fphe_ctx* ctx = NULL;

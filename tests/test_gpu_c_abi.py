@@ -29,3 +29,29 @@ def test_c_program_matches_fixture(bits):
     rows = [ln.split() for ln in out.stdout.strip().splitlines()]
     assert [int(c, 16) for c, _ in rows] == [int(c, 16) for c in e["ct"]]
     assert [int(d, 16) for _, d in rows] == [int(d, 16) for d in e["dec"]]
+
+
+def test_c_program_4096_vs_gmp():
+    """The same native consumer on a 4096-bit key (the TPI-8 geometry, L2 = 256): injected-r
+    encryptions of 64 encoded floats checked against libgmp (oracle/gmp_ref.c, the mpz_* call
+    sequence of paillier/src/lib.rs:104-121) and the CRT decryptions against the significands."""
+    import random
+    from oracle import gmp_ref
+    from oracle import paillier_oracle as O
+    if not os.path.exists(BIN):
+        raise RuntimeError("tests/c_abi/abi_roundtrip is not built (__graft_entry__.build())")
+    with open(os.path.join(HERE, "golden", "key_4096.json")) as f:
+        k = json.load(f)
+    p, q = int(k["p"], 16), int(k["q"], 16)
+    n = p * q
+    rng = random.Random(4096)
+    sigs = [O.encode_f64(n, rng.uniform(-1e6, 1e6)).significant for _ in range(64)]
+    rs = [1 + rng.randrange(n - 1) for _ in sigs]
+    lines = ["4096", hex(n), format(p, "x"), format(q, "x"), str(len(sigs))]
+    lines += [f"{format(s, 'x')} {format(r, 'x')}" for s, r in zip(sigs, rs)]
+    out = subprocess.run([BIN], input="\n".join(lines) + "\n", capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    rows = [ln.split() for ln in out.stdout.strip().splitlines()]
+    gk = gmp_ref.GmpKey(n, p, q)
+    assert [int(c, 16) for c, _ in rows] == [gk.encrypt(s, r, True) for s, r in zip(sigs, rs)]
+    assert [int(d, 16) for _, d in rows] == [s % n for s in sigs]
