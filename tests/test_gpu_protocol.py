@@ -31,12 +31,15 @@ def fixture_keys(bits):
     return (PR.SK(sk), PR.PK(pk), PR.Coder(coder)), O.keypair_from_primes(p, q)[1]
 
 
-@pytest.fixture(scope="module", params=["keygen1024", "fixture2048"])
+@pytest.fixture(scope="module", params=["keygen1024", "fixture2048", "keygen3072"])
 def keys(request):
     # the reference's tests use keygen(1024) (test_vertor_paillier.py:12); 2048 is the
-    # BASELINE key size
+    # BASELINE key size; 3072 runs the 4096-bit geometry (he_param.key_length is a job
+    # parameter)
     if request.param == "keygen1024":
         return PR.keygen(1024)
+    if request.param == "keygen3072":
+        return PR.keygen(3072)
     return fixture_keys(2048)[0]
 
 
