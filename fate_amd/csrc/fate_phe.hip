@@ -512,6 +512,11 @@ struct fphe_ctx {
   // two streams never share the window tables / intermediates at the same time
   hipStream_t scratch_stream = nullptr;
   bool scratch_used = false;
+  // a non-blocking side stream and its fork/join events (created on first use):
+  // fphe_fold_segments copies the source to element-major rows there while the call's
+  // stream reads back the exponent range and sorts the terms
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   std::mutex mu;
 };
 
@@ -768,6 +773,35 @@ struct CallBufs {
 
 constexpr size_t kMaxFoldKeys = (size_t)1 << 25;  // (segment, exponent) buckets per call
 
+fphe_status ensure_side(fphe_ctx* c) {
+  if (c->side) return FPHE_OK;
+  if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) {
+    c->side = nullptr;
+    return FPHE_ERR_HIP;
+  }
+  if (hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess)
+    return FPHE_ERR_HIP;
+  return FPHE_OK;
+}
+
+// Joins work forked onto the context's side stream back into the call's stream when the
+// call returns, on every path: declared after the call's CallBufs, it runs first, so the
+// stream-ordered frees of the call's scratch come after the side work.
+struct SideJoin {
+  fphe_ctx* c;
+  hipStream_t s;
+  bool armed = false;
+  ~SideJoin() {
+    if (armed) (void)hipStreamWaitEvent(s, c->ev_join, 0);
+  }
+  fphe_status join() {
+    if (!armed) return FPHE_OK;
+    armed = false;
+    return hip_ok(hipStreamWaitEvent(s, c->ev_join, 0));
+  }
+};
+
 // exclusive scan of n int32 on the device (3 launches); the total lands in *total if given
 fphe_status dev_scan(const fphe_ctx* c, const int32_t* in, size_t n, int32_t* out, int32_t* total, CallBufs& B) {
   const size_t nb = (n + kScanTile - 1) / kScanTile;
@@ -905,9 +939,24 @@ fphe_status launch_fold_segments(fphe_ctx* c, const u32* Src, const u8* ssign, c
   const unsigned g0 = gr_grid(nseg * FPHE_WAVE, c->cus);
   hipLaunchKernelGGL(k_gr_init_out<L>, dim3(g0), dim3(kGrBlock), 0, s, nseg, Co, so, eo, present);
   if (T == 0) return hip_ok(hipGetLastError());
-  // 1. exponent range (one small read back: it sizes the key space)
+  // 1. element-major copy of the source (the fold gathers whole rows), on the context's side
+  // stream: it overlaps the exponent-range read-back and the counting sort below, and the
+  // stream joins it before the fold (or on any early return, before the scratch is freed)
   int32_t* mm = B.get<int32_t>(4);
+  u32* rows = B.get<u32>(nsrc * L);
   if (!B.ok) return FPHE_ERR_HIP;
+  SideJoin sj{c, s};
+  if (ensure_side(c) != FPHE_OK || hipEventRecord(c->ev_fork, s) != hipSuccess ||
+      hipStreamWaitEvent(c->side, c->ev_fork, 0) != hipSuccess)
+    return FPHE_ERR_HIP;
+  hipLaunchKernelGGL(k_tiles_to_rows<L>, dim3((unsigned)std::min<size_t>(ntiles_of(nsrc), (size_t)c->cus * 8)),
+                     dim3(kGrBlock), 0, c->side, Src, nsrc, rows);
+  if (hipEventRecord(c->ev_join, c->side) != hipSuccess) {
+    (void)hipStreamSynchronize(c->side);
+    return FPHE_ERR_HIP;
+  }
+  sj.armed = true;
+  // 2. exponent range (one small read back: it sizes the key space)
   const int32_t mm0[4] = {kI32Max, kI32Min, 0, 0};
   if (hipMemcpyAsync(mm, mm0, sizeof(mm0), hipMemcpyHostToDevice, s) != hipSuccess) return FPHE_ERR_HIP;
   hipLaunchKernelGGL(k_gr_minmax, dim3(gr_grid(T, c->cus)), dim3(kGrBlock), 0, s, idx, seg, sexp, T, nsrc, nseg, mm);
@@ -922,8 +971,6 @@ fphe_status launch_fold_segments(fphe_ctx* c, const u32* Src, const u8* ssign, c
   // copies against atomic contention on hot keys (k_gr_keys), while they stay small
   const bool lds_counts = nkeys <= kBcMaxKeys;
   const int32_t R = lds_counts ? 1 : (nkeys <= ((size_t)1 << 22) ? 8 : 1);
-  // 2. element-major copy of the source (the fold gathers whole rows)
-  u32* rows = B.get<u32>(nsrc * L);
   int32_t* keys = B.get<int32_t>(T);
   int32_t* cntR = B.get<int32_t>(nkeys * R);
   int32_t* offR = B.get<int32_t>(nkeys * R);
@@ -933,8 +980,6 @@ fphe_status launch_fold_segments(fphe_ctx* c, const u32* Src, const u8* ssign, c
   int32_t* ord = B.get<int32_t>(T);
   int32_t* skey = B.get<int32_t>(T);
   if (!B.ok) return FPHE_ERR_HIP;
-  hipLaunchKernelGGL(k_tiles_to_rows<L>, dim3((unsigned)std::min<size_t>(ntiles_of(nsrc), (size_t)c->cus * 8)),
-                     dim3(kGrBlock), 0, s, Src, nsrc, rows);
   // 3. keys, counts, counting sort
   if (hipMemsetAsync(cntR, 0, nkeys * R * 4, s) != hipSuccess || hipMemsetAsync(fill, 0, nkeys * R * 4, s) != hipSuccess ||
       hipMemsetAsync(last, 0xff, nseg * 4, s) != hipSuccess || hipMemsetAsync(litseg, 0, nseg, s) != hipSuccess)
@@ -989,7 +1034,7 @@ fphe_status launch_fold_segments(fphe_ctx* c, const u32* Src, const u8* ssign, c
   P.sign = B.get<u8>(ub1);
   P.exp = B.get<int32_t>(ub1);
   P.key = B.get<int32_t>(ub1);
-  if (!B.ok) return FPHE_ERR_HIP;
+  if (!B.ok || sj.join() != FPHE_OK) return FPHE_ERR_HIP;
   hipLaunchKernelGGL(ksf, dim3(occ_grid(c, ksf, lds, (nslots + E - 1) / E, "segfold")), dim3(kBlock), lds, s, c->K,
                      rows, ssign, sexp, ord, skey, T, (u32)r, poff, c->K.FR_27, P.rows, P.sign, P.exp, P.key, (u32)NL);
   P.cnt = cnt2;
@@ -1632,6 +1677,9 @@ fphe_status fphe_ctx_destroy(fphe_ctx* c) {
     DevGuard g(c->device);
     if (c->blob) (void)hipFree(c->blob);
     if (c->scratch) (void)hipFree(c->scratch);
+    if (c->side) (void)hipStreamDestroy(c->side);
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   }
   delete c;
   return FPHE_OK;
