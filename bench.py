@@ -237,7 +237,8 @@ def add_kernel_leg(P, pk, a, b, N, stream, dev) -> dict:
     def launch():
         _lib.check(lib.fphe_add_ordered(ctx, P._ptr(a.C), P._ptr(a.sign), P._ptr(a.exp), P._ptr(b.C), P._ptr(b.sign),
                                         P._ptr(b.exp), 1, N, P._ptr(order), P._ptr(out.C), P._ptr(out.sign),
-                                        P._ptr(out.exp), ctypes.c_void_p(stream.cuda_stream)), "fphe_add_ordered")
+                                        P._ptr(out.exp), None, ctypes.c_void_p(stream.cuda_stream)),
+                   "fphe_add_ordered")
 
     launch()  # warm-up
     ev = []
@@ -253,7 +254,8 @@ def add_kernel_leg(P, pk, a, b, N, stream, dev) -> dict:
     L = a.L2
     mac = N * (1 + 4 * float(gaps.double().mean())) * mac32_per_mont(L)
     hist = torch.bincount(gaps.cpu()).tolist()
-    # issued MACs: to-Montgomery + final product (general) and the wave-max squarings
+    # issued MACs: the final product (general; Montgomery-resident operands need no
+    # to-Montgomery product) and the wave-max squarings
     TPI = L // 32
     NL = ENGINE_LL * TPI
     per_wave = 64 // TPI
@@ -262,7 +264,7 @@ def add_kernel_leg(P, pk, a, b, N, stream, dev) -> dict:
     if pad:
         gs = torch.cat([gs, gs.new_zeros(pad)])
     wave_sq = 4 * gs.view(-1, per_wave).amax(1).double().sum().item() * per_wave
-    mads = N * 2 * 2 * NL * NL + wave_sq * NL * TPI * (ENGINE_LL // 2 + 1 + ENGINE_LL)
+    mads = N * 2 * NL * NL + wave_sq * NL * TPI * (ENGINE_LL // 2 + 1 + ENGINE_LL)
     blk = valu_roofline("k_add27<128> (exponent-gap order)", mac, ms, N * (3 * (L * 4 + 5) + 4),
                         per_elem_mac32=round(mac / N, 1), gap_histogram=hist, sorted=order is not None)
     blk["issue"] = {"mad64_per_elem": round(mads / N, 1), "achieved": round(mads / (ms / 1e3) / 1e12, 3),
@@ -562,16 +564,19 @@ def main() -> None:
         torch.cuda.synchronize(dev)
         add_ms = e0.elapsed_time(e1)
         add_kernel = add_kernel_leg(P, pk, ct, ct2, N, stream, dev)
-        # end-to-end from host f32 to host ciphertexts (pinned), one pass
+        # end-to-end from host f32 to the reference's signed ciphertext integers in pinned host
+        # memory (export out of the Montgomery-resident form included), one pass
         xh = x.pin_memory()
+        Ch = torch.empty((N, ct.L2), dtype=torch.int32, pin_memory=True)
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         ce = pk.encrypt_encoded(coder.encode_f32_vec(xh.to(dev, non_blocking=True)), True)
-        Ch = torch.empty(ce.C.shape, dtype=ce.C.dtype, pin_memory=True)
-        Ch.copy_(ce.C, non_blocking=True)
-        sh = ce.sign.cpu(); eh = ce.exp.cpu()
+        mag_e, neg_e, exp_e = ce.export_signed(pk)
+        Ch.copy_(mag_e, non_blocking=True)
+        sh = neg_e.cpu(); eh = exp_e.cpu()
         torch.cuda.synchronize(dev)
         e2e = time.perf_counter() - t0
+        del mag_e, neg_e, exp_e
         # ct x pt (SecureBoost GOSS-style weights; negatives take the device inverse branch)
         gw = torch.Generator().manual_seed(777 + rank)
         wts = (torch.rand(N, generator=gw, dtype=torch.float32) * 3.0 - 1.0).to(dev)

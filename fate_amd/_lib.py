@@ -32,7 +32,7 @@ EF_EXP_RANGE = 0x40
 
 # every symbol declared in include/fate_phe.h
 EXPORTED_SYMBOLS = (
-    "fphe_ctx_create", "fphe_ctx_destroy", "fphe_ctx_limbs",
+    "fphe_ctx_create", "fphe_ctx_destroy", "fphe_ctx_limbs", "fphe_ctx_mont_one",
     "fphe_encode_f32", "fphe_encode_f64", "fphe_decode_f32", "fphe_decode_f64",
     "fphe_encode_i64", "fphe_decode_i64", "fphe_decode_i32", "fphe_pack_f64", "fphe_unpack_f64",
     "fphe_encrypt", "fphe_encrypt_crt", "fphe_decrypt", "fphe_add", "fphe_add_ordered", "fphe_add_order", "fphe_mul", "fphe_neg", "fphe_sqmul", "fphe_align",
@@ -68,6 +68,8 @@ def load() -> ctypes.CDLL:
         lib.fphe_ctx_destroy.restype = st
         lib.fphe_ctx_limbs.argtypes = [vp, c_u32p, c_u32p]
         lib.fphe_ctx_limbs.restype = st
+        lib.fphe_ctx_mont_one.argtypes = [vp, c_u32p]
+        lib.fphe_ctx_mont_one.restype = st
         for name in ("fphe_encode_f32", "fphe_encode_f64"):
             f = getattr(lib, name)
             f.argtypes = [vp, vp, ctypes.c_size_t, vp, vp, vp, vp, vp]
@@ -96,10 +98,10 @@ def load() -> ctypes.CDLL:
         lib.fphe_encrypt_crt.restype = st
         lib.fphe_decrypt.argtypes = [vp, vp, ctypes.c_size_t, vp, vp]
         lib.fphe_decrypt.restype = st
-        lib.fphe_add.argtypes = [vp, vp, vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_size_t, vp, vp, vp, vp]
+        lib.fphe_add.argtypes = [vp, vp, vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_size_t, vp, vp, vp, vp, vp]
         lib.fphe_add.restype = st
         lib.fphe_add_ordered.argtypes = [vp, vp, vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_size_t, vp, vp, vp, vp,
-                                         vp]
+                                         vp, vp]
         lib.fphe_add_ordered.restype = st
         lib.fphe_mul.argtypes = [vp, vp, vp, vp, vp, ctypes.c_uint32, vp, vp, ctypes.c_int, ctypes.c_size_t,
                                  vp, vp, vp, vp, vp]

@@ -64,7 +64,12 @@ struct KeyArgs {
   const u32* ep; const u32* eq;          // n mod p(p-1), n mod q(q-1)           [L1]
   int ep_bits, eq_bits;
   const u32* KpR_27; const u32* KqR_27;  // Kp R, Kq R mod n^2 (R = 2^(LB NL2))         [NL2]
-  const u32* FR_27;                      // R^k mod n^2, k = 0..kFoldFR                [kFoldFR+1][NL2]
+  // Montgomery-resident ciphertexts: vectors hold M(c) = c R mod n^2 with the
+  // n^2 engine's R.  R^3 mod n^2 takes a plain value x to x R^2 in one product (inverses,
+  // the key-holder nude factor); R_s^2 R^-1 mod s^2 takes M(c) mod s^2 to c R_s (decrypt).
+  const u32* N2R3_27;                    // R^3 mod n^2                                  [NL2]
+  const u32* P2RX_27; const u32* Q2RX_27;  // R_s^2 R^-1 mod s^2, s = p, q                [NLh]
+  const u32* N2M1;                       // M(1) = R mod n^2 in 32-bit words (literal 1)  [L2]
 };
 
 __device__ __forceinline__ void set_err(int32_t* err, u32 f) {
@@ -727,7 +732,7 @@ fphe_status launch_fold27(fphe_ctx* c, const uint32_t* Src, const uint8_t* ssign
   set_lds(kern, lds);
   const unsigned grid = occ_grid(c, kern, lds, (nchunks + E - 1) / E, "fold27");
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, Src, ssign, sexp, ord, cstart, clen, nchunks,
-                     (const int32_t*)nullptr, (const int32_t*)nullptr, (u32*)nullptr, c->K.FR_27, Co, so, eo, (u32)NL);
+                     (const int32_t*)nullptr, (const int32_t*)nullptr, (u32*)nullptr, Co, so, eo, (u32)NL);
   return hip_ok(hipGetLastError());
 }
 
@@ -909,7 +914,7 @@ fphe_status fold_level(fphe_ctx* c, FoldLevel& in, FoldOut& out, CallBufs& B, bo
   set_lds(kern, lds);
   const unsigned grid = occ_grid(c, kern, lds, (ub + E - 1) / E, "fold_segments");
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, in.rows, in.sign, in.exp, in.ord, cstart, clen,
-                     ub, (const int32_t*)(hdr + 2), (const int32_t*)cperm, ctr, c->K.FR_27, out.rows, out.sign, out.exp,
+                     ub, (const int32_t*)(hdr + 2), (const int32_t*)cperm, ctr, out.rows, out.sign, out.exp,
                      (u32)NL);
   out.cnt = nch;
   out.off = choff;
@@ -937,7 +942,7 @@ fphe_status launch_fold_segments(fphe_ctx* c, const u32* Src, const u8* ssign, c
   constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = rad_ll(TPI) * TPI;
   CallBufs B(s);
   const unsigned g0 = gr_grid(nseg * FPHE_WAVE, c->cus);
-  hipLaunchKernelGGL(k_gr_init_out<L>, dim3(g0), dim3(kGrBlock), 0, s, nseg, Co, so, eo, present);
+  hipLaunchKernelGGL(k_gr_init_out<L>, dim3(g0), dim3(kGrBlock), 0, s, nseg, c->K.N2M1, Co, so, eo, present);
   if (T == 0) return hip_ok(hipGetLastError());
   // 1. element-major copy of the source (the fold gathers whole rows), on the context's side
   // stream: it overlaps the exponent-range read-back and the counting sort below, and the
@@ -1010,7 +1015,7 @@ fphe_status launch_fold_segments(fphe_ctx* c, const u32* Src, const u8* ssign, c
   set_lds(ksf, lds);
   const size_t round = (size_t)occ_grid(c, ksf, lds, (size_t)1 << 40, "segfold") * kWavesPerBlock * E;
   size_t r = (T + round - 1) / round;
-  r = r < 8 ? 8 : (r > (size_t)kFoldFR ? (size_t)kFoldFR : r);
+  r = r < 8 ? 8 : (r > (size_t)kSegFoldMax ? (size_t)kSegFoldMax : r);
   const size_t nslots = (T + r - 1) / r;
   int32_t* pcnt = B.get<int32_t>(nslots);
   int32_t* poff = B.get<int32_t>(nslots);
@@ -1036,7 +1041,7 @@ fphe_status launch_fold_segments(fphe_ctx* c, const u32* Src, const u8* ssign, c
   P.key = B.get<int32_t>(ub1);
   if (!B.ok || sj.join() != FPHE_OK) return FPHE_ERR_HIP;
   hipLaunchKernelGGL(ksf, dim3(occ_grid(c, ksf, lds, (nslots + E - 1) / E, "segfold")), dim3(kBlock), lds, s, c->K,
-                     rows, ssign, sexp, ord, skey, T, (u32)r, poff, c->K.FR_27, P.rows, P.sign, P.exp, P.key, (u32)NL);
+                     rows, ssign, sexp, ord, skey, T, (u32)r, poff, P.rows, P.sign, P.exp, P.key, (u32)NL);
   P.cnt = cnt2;
   P.off = off2;
   P.n_dev = hdr + 2;
@@ -1064,7 +1069,7 @@ fphe_status launch_fold_segments(fphe_ctx* c, const u32* Src, const u8* ssign, c
       return FPHE_ERR_HIP;
     const unsigned gp = gr_grid(np, c->cus);
     hipLaunchKernelGGL(k_gr_segmin<L>, dim3(gp), dim3(kGrBlock), 0, s, P.rows, P.sign, P.exp, P.key, P.n_dev,
-                       (int32_t)NE, segmin, lit);
+                       (int32_t)NE, c->K.N2M1, segmin, lit);
     hipLaunchKernelGGL(k_gr_gaps, dim3(gp), dim3(kGrBlock), 0, s, P.exp, P.key, lit, P.n_dev, (int32_t)NE, segmin, gap,
                        skey, scnt, gh, err);
     // partials in descending-gap order (counting sort on NE - 1 - gap: every gap < NE), then
@@ -1098,7 +1103,7 @@ fphe_status launch_fold_segments(fphe_ctx* c, const u32* Src, const u8* ssign, c
   }
   // 6. scatter to the output segments (keys are segment ids here)
   hipLaunchKernelGGL(k_gr_final<L>, dim3(gr_grid(P.n_ub * 64, c->cus)), dim3(kGrBlock), 0, s, P.rows, P.sign, P.exp,
-                     P.key, P.n_dev, litseg, Co, so, eo, present);
+                     P.key, P.n_dev, c->K.N2M1, litseg, Co, so, eo, present);
   // literal-1 results end on their segment's last term's exponent
   hipLaunchKernelGGL(k_gr_last, dim3(gr_grid(T, c->cus)), dim3(kGrBlock), 0, s, seg, T, litseg, last);
   hipLaunchKernelGGL(k_gr_litexp, dim3(gr_grid(nseg, c->cus)), dim3(kGrBlock), 0, s, nseg, litseg, last, idx, sexp, eo);
@@ -1114,7 +1119,7 @@ size_t add_max_count(int L) {
 template <int L>
 fphe_status launch_add27(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, const int32_t* ea, const uint32_t* Cb,
                          const uint8_t* sb, const int32_t* eb, int bstride, size_t count, const int32_t* ord,
-                         uint32_t* Co, uint8_t* so, int32_t* eo, hipStream_t s) {
+                         uint32_t* Co, uint8_t* so, int32_t* eo, int32_t* err, hipStream_t s) {
   constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = rad_ll(TPI) * TPI;
   auto kern = KS<TPI>::template add<L>();
   const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
@@ -1135,7 +1140,7 @@ fphe_status launch_add27(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, con
     if (hipMemsetAsync(next_tile, 0, kCtrBytes, s) != hipSuccess) return FPHE_ERR_HIP;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, Ca + wo, sa + s0, ea + s0,
                        bstride ? Cb + wo : Cb, bstride ? sb + s0 : sb, bstride ? eb + s0 : eb, bstride, n, ord,
-                       Co + wo, so + s0, eo + s0, next_tile, (u32)NL);
+                       Co + wo, so + s0, eo + s0, err, next_tile, (u32)NL);
   }
   return hip_ok(hipGetLastError());
 }
@@ -1149,6 +1154,18 @@ fphe_status launch_sqmul27(fphe_ctx* c, const uint32_t* Ca, const uint32_t* Cb, 
   set_lds(kern, lds);
   const unsigned grid = occ_grid(c, kern, lds, (count + E - 1) / E, "sqmul27");
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, Ca, Cb, sb, nsq, count, Co, so, (u32)NL);
+  return hip_ok(hipGetLastError());
+}
+
+template <int L>
+fphe_status launch_mont_const27(fphe_ctx* c, const uint32_t* C, size_t count, const u32* X, uint32_t* Co,
+                                hipStream_t s) {
+  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = rad_ll(TPI) * TPI;
+  auto kern = KS<TPI>::template mont_const<L>();
+  const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
+  set_lds(kern, lds);
+  const unsigned grid = occ_grid(c, kern, lds, (count + E - 1) / E, "mont_const27");
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, C, count, X, Co, (u32)NL);
   return hip_ok(hipGetLastError());
 }
 
@@ -1546,20 +1563,8 @@ fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, 
     const size_t o_N2_27 = put(to27(N2, NL2, LB2), NL2);
     const size_t o_N2R1_27 = put(to27(hbn::pow2_mod((size_t)LB2 * NL2, N2), NL2, LB2), NL2);
     const size_t o_N2R2_27 = put(to27(hbn::pow2_mod((size_t)2 * LB2 * NL2, N2), NL2, LB2), NL2);
-    // R^k mod n^2, k = 0..kFoldFR (28-bit limbs): the fold kernels' fix-up factors
-    size_t o_FR = 0;
-    {
-      // rows of exactly NL2 limbs, back to back (k_fold27 indexes row k at k * NL): one put,
-      // since put() pads each section to 16 bytes and NL2 = 74 is not a multiple of 4
-      const Limbs R27 = hbn::pow2_mod((size_t)LB2 * NL2, N2);
-      Limbs x{1}, rows;
-      for (int k = 0; k <= kFoldFR; ++k) {
-        const Limbs r = to27(x, NL2, LB2);
-        rows.insert(rows.end(), r.begin(), r.end());
-        x = hbn::mod(hbn::mul(x, R27), N2);
-      }
-      o_FR = put(rows, rows.size());
-    }
+    const size_t o_N2R3_27 = put(to27(hbn::pow2_mod((size_t)3 * LB2 * NL2, N2), NL2, LB2), NL2);
+    const size_t o_N2M1 = put(hbn::pow2_mod((size_t)LB2 * NL2, N2), L2);
     const size_t o_Nn_27 = put(to27(n, NLh, LBh), NLh);
     const size_t o_NnR1_27 = put(to27(hbn::pow2_mod((size_t)LBh * NLh, n), NLh, LBh), NLh);
     const size_t o_NnR2_27 = put(to27(hbn::pow2_mod((size_t)2 * LBh * NLh, n), NLh, LBh), NLh);
@@ -1568,7 +1573,7 @@ fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, 
     size_t o_Q2 = 0, o_Q2R3 = 0, o_qm1 = 0, o_q = 0, o_qinv2 = 0, o_hqR = 0, o_pinvqR = 0;
     u32 p2n0 = 0, pn0 = 0, q2n0 = 0, qn0 = 0;
     int pm1b = 0, qm1b = 0, epb = 0, eqb = 0;
-    size_t o_ep = 0, o_eq = 0, o_KpR = 0, o_KqR = 0;
+    size_t o_ep = 0, o_eq = 0, o_KpR = 0, o_KqR = 0, o_P2RX_27 = 0, o_Q2RX_27 = 0;
     const bool has_sk = p_w != nullptr;
     if (has_sk) {
       Limbs p = from_words(p_w, LQ), q = from_words(q_w, LQ);
@@ -1605,6 +1610,13 @@ fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, 
       o_Q2_27 = put(to27(Q2, NLh, LBh), NLh);
       o_Q2R1_27 = put(to27(hbn::pow2_mod((size_t)LBh * NLh, Q2), NLh, LBh), NLh);
       o_Q2R2_27 = put(to27(hbn::pow2_mod((size_t)2 * LBh * NLh, Q2), NLh, LBh), NLh);
+      // R_s^2 R^-1 mod s^2 (R of n^2, R_s of s^2): mont_s(M(c) mod s^2, .) = c R_s
+      auto rx = [&](const Limbs& S2) {
+        const Limbs Rn = hbn::pow2_mod((size_t)LB2 * NL2, S2);
+        return hbn::mod(hbn::mul(hbn::pow2_mod((size_t)2 * LBh * NLh, S2), hbn::inv_mod(Rn, S2)), S2);
+      };
+      o_P2RX_27 = put(to27(rx(P2), NLh, LBh), NLh);
+      o_Q2RX_27 = put(to27(rx(Q2), NLh, LBh), NLh);
       p2n0 = hbn::neg_inv32(P2[0]); pn0 = hbn::neg_inv32(p[0]);
       q2n0 = hbn::neg_inv32(Q2[0]); qn0 = hbn::neg_inv32(q[0]);
       pm1b = (int)hbn::bitlen(pm1); qm1b = (int)hbn::bitlen(qm1);
@@ -1648,7 +1660,8 @@ fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, 
     K.nbits = (int)key_bits;
     K.N2_27 = b + o_N2_27; K.N2R1_27 = b + o_N2R1_27; K.N2R2_27 = b + o_N2R2_27;
     K.n2_np27 = K.n2_n0inv & ((1u << LB2) - 1u);
-    K.FR_27 = b + o_FR;
+    K.N2R3_27 = b + o_N2R3_27;
+    K.N2M1 = b + o_N2M1;
     K.Nn_27 = b + o_Nn_27; K.NnR1_27 = b + o_NnR1_27; K.NnR2_27 = b + o_NnR2_27;
     K.nn_np27 = hbn::neg_inv32(n[0]) & ((1u << LBh) - 1u);
     K.nn_inv27 = (0u - hbn::neg_inv32(n[0])) & ((1u << LBh) - 1u);
@@ -1663,6 +1676,7 @@ fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, 
       K.p2_np27 = p2n0 & ((1u << LBh) - 1u); K.q2_np27 = q2n0 & ((1u << LBh) - 1u);
       K.ep = b + o_ep; K.eq = b + o_eq; K.ep_bits = epb; K.eq_bits = eqb;
       K.KpR_27 = b + o_KpR; K.KqR_27 = b + o_KqR;
+      K.P2RX_27 = b + o_P2RX_27; K.Q2RX_27 = b + o_Q2RX_27;
     }
     *out = c;
     return FPHE_OK;
@@ -1925,17 +1939,18 @@ fphe_status fphe_decrypt(fphe_ctx* c, const uint32_t* C, size_t count, uint32_t*
 
 fphe_status fphe_add_ordered(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, const int32_t* ea,
                              const uint32_t* Cb, const uint8_t* sb, const int32_t* eb, int b_stride, size_t count,
-                             const int32_t* order, uint32_t* Co, uint8_t* so, int32_t* eo, void* stream) {
+                             const int32_t* order, uint32_t* Co, uint8_t* so, int32_t* eo, int32_t* err,
+                             void* stream) {
   if (!c) return FPHE_ERR_ARG;
   if (count == 0) return FPHE_OK;
   if (!Ca || !sa || !ea || !Cb || !sb || !eb || !Co || !so || !eo) return FPHE_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DevGuard g(c->device);
   if (c->L2 == 256)
-    return launch_add27<256>(c, Ca, sa, ea, Cb, sb, eb, b_stride, count, order, Co, so, eo, (hipStream_t)stream);
+    return launch_add27<256>(c, Ca, sa, ea, Cb, sb, eb, b_stride, count, order, Co, so, eo, err, (hipStream_t)stream);
   if (c->L2 == 128)
-    return launch_add27<128>(c, Ca, sa, ea, Cb, sb, eb, b_stride, count, order, Co, so, eo, (hipStream_t)stream);
-  return launch_add27<64>(c, Ca, sa, ea, Cb, sb, eb, b_stride, count, order, Co, so, eo, (hipStream_t)stream);
+    return launch_add27<128>(c, Ca, sa, ea, Cb, sb, eb, b_stride, count, order, Co, so, eo, err, (hipStream_t)stream);
+  return launch_add27<64>(c, Ca, sa, ea, Cb, sb, eb, b_stride, count, order, Co, so, eo, err, (hipStream_t)stream);
 }
 
 fphe_status fphe_add_order(const int32_t* ea, const int32_t* eb, size_t count, uint32_t L2, int32_t* order,
@@ -1961,8 +1976,8 @@ fphe_status fphe_add_order(const int32_t* ea, const int32_t* eb, size_t count, u
 
 fphe_status fphe_add(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, const int32_t* ea, const uint32_t* Cb,
                      const uint8_t* sb, const int32_t* eb, int b_stride, size_t count, uint32_t* Co, uint8_t* so,
-                     int32_t* eo, void* stream) {
-  return fphe_add_ordered(c, Ca, sa, ea, Cb, sb, eb, b_stride, count, nullptr, Co, so, eo, stream);
+                     int32_t* eo, int32_t* err, void* stream) {
+  return fphe_add_ordered(c, Ca, sa, ea, Cb, sb, eb, b_stride, count, nullptr, Co, so, eo, err, stream);
 }
 
 
@@ -2068,9 +2083,20 @@ fphe_status fphe_export_signed(fphe_ctx* c, const uint32_t* C, const uint8_t* si
   if (!c) return FPHE_ERR_ARG;
   if (count == 0) return FPHE_OK;
   if (!C || !sign || !mag || !neg) return FPHE_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
   DevGuard g(c->device);
-  hipLaunchKernelGGL(k_export_signed, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                     c->K.N2, (u32)c->L2, C, sign, count, mag, neg);
+  hipStream_t s = (hipStream_t)stream;
+  // out of the Montgomery-resident form into a stream-ordered scratch vector, then the
+  // reference's signed integers
+  CallBufs B(s);
+  u32* plain = B.get<u32>((size_t)ntiles_of(count) * c->L2 * FPHE_WAVE);
+  if (!B.ok) return FPHE_ERR_HIP;
+  fphe_status st = c->L2 == 256   ? launch_mont_const27<256>(c, C, count, nullptr, plain, s)
+                   : c->L2 == 128 ? launch_mont_const27<128>(c, C, count, nullptr, plain, s)
+                                  : launch_mont_const27<64>(c, C, count, nullptr, plain, s);
+  if (st != FPHE_OK) return st;
+  hipLaunchKernelGGL(k_export_signed, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, s, c->K.N2, (u32)c->L2,
+                     plain, sign, count, mag, neg);
   return hip_ok(hipGetLastError());
 }
 
@@ -2079,10 +2105,21 @@ fphe_status fphe_import_signed(fphe_ctx* c, const uint32_t* mag, const uint8_t* 
   if (!c) return FPHE_ERR_ARG;
   if (count == 0) return FPHE_OK;
   if (!C || !sign || !mag || !neg) return FPHE_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
   DevGuard g(c->device);
-  hipLaunchKernelGGL(k_import_signed, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                     c->K.N2, (u32)c->L2, mag, neg, count, C, sign);
-  return hip_ok(hipGetLastError());
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_import_signed, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, s, c->K.N2, (u32)c->L2, mag,
+                     neg, count, C, sign);
+  // into the Montgomery-resident form, in place
+  return c->L2 == 256   ? launch_mont_const27<256>(c, C, count, c->K.N2R2_27, C, s)
+         : c->L2 == 128 ? launch_mont_const27<128>(c, C, count, c->K.N2R2_27, C, s)
+                        : launch_mont_const27<64>(c, C, count, c->K.N2R2_27, C, s);
+}
+
+fphe_status fphe_ctx_mont_one(const fphe_ctx* c, uint32_t* one) {
+  if (!c || !one) return FPHE_ERR_ARG;
+  DevGuard g(c->device);
+  return hip_ok(hipMemcpy(one, c->K.N2M1, (size_t)c->L2 * 4, hipMemcpyDeviceToHost));
 }
 
 

@@ -365,17 +365,19 @@ __global__ __launch_bounds__(kGrBlock) void k_gr_chunks(const int32_t* __restric
 
 // --- exponent merge ---------------------------------------------------------------------------------
 // Per final (segment, exponent) partial p (element-major rows, L words): literal-1 test (the
-// reference's zero: signed integer exactly 1) and the segment's least non-literal exponent.
+// reference's zero: signed integer exactly 1, stored as M(1) = `one`) and the segment's least
+// non-literal exponent.
 template <int L>
 __global__ __launch_bounds__(kGrBlock) void k_gr_segmin(const u32* __restrict__ rows, const u8* __restrict__ sign,
                                                         const int32_t* __restrict__ exp, const int32_t* __restrict__ pkey,
                                                         const int32_t* __restrict__ np_dev, int32_t NE,
-                                                        int32_t* __restrict__ segmin, u8* __restrict__ lit) {
+                                                        const u32* __restrict__ one, int32_t* __restrict__ segmin,
+                                                        u8* __restrict__ lit) {
   const int32_t np = *np_dev;
   for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < (size_t)np; p += (size_t)gridDim.x * blockDim.x) {
     const u32* r = rows + p * L;
-    u32 acc = r[0] ^ 1u;
-    for (int j = 1; j < L; ++j) acc |= r[j];
+    u32 acc = 0;
+    for (int j = 0; j < L; ++j) acc |= r[j] ^ one[j];
     const bool one = acc == 0 && sign[p] == 0;
     lit[p] = one ? 1 : 0;
     if (!one) atomicMin(&segmin[pkey[p] / NE], exp[p]);
@@ -445,15 +447,17 @@ __global__ __launch_bounds__(kGrBlock) void k_tiles_to_rows(const u32* __restric
 }
 
 // Final scatter: out[seg] (tile-major) for every segment: the segment's folded partial, or the
-// literal 1 (exp 0) for a segment without terms.  A literal-1 result takes the exponent of the
-// segment's last term (the reference's sequential fold ends on it, lib.rs:303-308).
+// literal 1 (exp 0, stored as M(1) = `one`) for a segment without terms.  A literal-1 result
+// takes the exponent of the segment's last term (the reference's sequential fold ends on it,
+// lib.rs:303-308).
 template <int L>
-__global__ __launch_bounds__(kGrBlock) void k_gr_init_out(size_t nseg, u32* __restrict__ Co, u8* __restrict__ so,
-                                                          int32_t* __restrict__ eo, u8* __restrict__ present) {
+__global__ __launch_bounds__(kGrBlock) void k_gr_init_out(size_t nseg, const u32* __restrict__ one, u32* __restrict__ Co,
+                                                          u8* __restrict__ so, int32_t* __restrict__ eo,
+                                                          u8* __restrict__ present) {
   const size_t nt = (nseg + FPHE_WAVE - 1) / FPHE_WAVE;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nt * L * FPHE_WAVE; i += (size_t)gridDim.x * blockDim.x) {
     const size_t w = (i >> 6) % L;
-    Co[i] = w == 0 ? 1u : 0u;
+    Co[i] = one[w];
   }
   for (size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x; s < nt * FPHE_WAVE; s += (size_t)gridDim.x * blockDim.x) {
     so[s] = 0;
@@ -465,9 +469,9 @@ __global__ __launch_bounds__(kGrBlock) void k_gr_init_out(size_t nseg, u32* __re
 template <int L>
 __global__ __launch_bounds__(kGrBlock) void k_gr_final(const u32* __restrict__ rows, const u8* __restrict__ sign,
                                                        const int32_t* __restrict__ exp, const int32_t* __restrict__ pkey,
-                                                       const int32_t* __restrict__ np_dev, u8* __restrict__ litseg,
-                                                       u32* __restrict__ Co, u8* __restrict__ so, int32_t* __restrict__ eo,
-                                                       u8* __restrict__ present) {
+                                                       const int32_t* __restrict__ np_dev, const u32* __restrict__ one,
+                                                       u8* __restrict__ litseg, u32* __restrict__ Co, u8* __restrict__ so,
+                                                       int32_t* __restrict__ eo, u8* __restrict__ present) {
   const int32_t np = *np_dev;
   // one wave per partial: lanes copy words, lane 0 the per-element fields
   const size_t lane = threadIdx.x & 63;
@@ -478,7 +482,7 @@ __global__ __launch_bounds__(kGrBlock) void k_gr_final(const u32* __restrict__ r
     u32 acc = 0;
     for (int j = (int)lane; j < L; j += 64) {
       const u32 v = r[j];
-      acc |= j == 0 ? (v ^ 1u) : v;
+      acc |= v ^ one[j];
       Co[(((size_t)s >> 6) * L + j) * FPHE_WAVE + (s & 63)] = v;
     }
     const bool one = __ballot(acc != 0) == 0 && sign[p] == 0;

@@ -105,9 +105,8 @@ __device__ __forceinline__ ColIO colio(const u32* tile_base, u32 rows, u32 col, 
 }
 
 constexpr int kFoldMax = 64;  // terms per k_fold27 chunk
-// R^k fix-up rows in the key blob, k = 0..kFoldFR: the chunk folds (k <= kFoldMax) and the
-// balanced first level (k_segfold27: runs of up to kFoldFR items per wave slot)
-constexpr int kFoldFR = 1024;
+// items per wave slot of the balanced first fold level (k_segfold27), at most
+constexpr int kSegFoldMax = 1024;
 // largest exponent gap k_add27 / k_align27 act on (4 kMaxGap squarings, ~7 s on one wave):
 // far beyond the reference encoders' exponent range (f64: [-282, 242]); fphe_align rejects
 // larger gaps on the host side (fate_amd/paillier.py), k_add27 caps them

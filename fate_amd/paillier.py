@@ -184,12 +184,24 @@ class _KeyCtx:
         self.L1 = 32 if self.key_bits <= 1024 else (64 if self.key_bits <= 2048 else 128)
         self.L2 = 2 * self.L1
         self._ctx: Dict[int, ctypes.c_void_p] = {}
+        self._one: Dict[int, torch.Tensor] = {}
         self._lock = threading.Lock()
         self.rng_key = (ctypes.c_uint32 * 8)(*np.frombuffer(os.urandom(32), dtype=np.uint32).tolist())
         self._nonce = itertools.count(1)
 
     def next_nonce(self) -> int:
         return (os.getpid() << 40) ^ next(self._nonce)
+
+    def mont_one(self, device: torch.device) -> torch.Tensor:
+        """M(1) = R mod n^2, the stored words of the literal 1 (int32 [L2] on `device`):
+        device vectors are Montgomery-resident (fphe_ctx_mont_one, include/fate_phe.h)."""
+        idx = device.index
+        t = self._one.get(idx)
+        if t is None:
+            w = (ctypes.c_uint32 * self.L2)()
+            _lib.check(_lib.load().fphe_ctx_mont_one(self.ctx(device), w), "fphe_ctx_mont_one")
+            t = self._one[idx] = torch.tensor(np.frombuffer(w, dtype=np.uint32).view(np.int32), device=device)
+        return t
 
     def ctx(self, device: torch.device) -> ctypes.c_void_p:
         idx = device.index
@@ -424,12 +436,14 @@ class Plaintext:
 
 class CiphertextVector:
     """Encrypted vector (``fixedpoint_paillier::CiphertextVector``, lib.rs:353-356):
-    C [ntiles, L2, 64] canonical residues mod n^2, sign (reference integer = C - n^2),
-    exp (base-16 exponent)."""
+    C [ntiles, L2, 64] the key's Montgomery-resident residues M(c) = c R mod n^2 of the
+    canonical ciphertexts c, sign (reference integer = c - n^2), exp (base-16 exponent).
+    Every product kernel works on M(.) directly (include/fate_phe.h)."""
 
-    # n: the key's modulus once known (set by encrypt and by every op that takes a PK);
-    # pickling needs it to write the reference's signed integers C - n^2.  raw: an unpickled
-    # vector not yet given its key (C = magnitudes, sign = negative flags; see _resolve)
+    # n: the key's modulus (set by encrypt and by every op that takes a PK); M(.) is
+    # meaningful under that key only, and pickling needs it to write the reference's signed
+    # integers.  raw: a key-less vector -- unpickled, or zeros() -- not yet given its key (C =
+    # magnitudes of the reference's signed integers, sign = negative flags; see _resolve)
     __slots__ = ("C", "sign", "exp", "count", "n", "raw")
 
     def __init__(self, C: torch.Tensor = None, sign: torch.Tensor = None, exp: torch.Tensor = None, count: int = 0,
@@ -462,37 +476,48 @@ class CiphertextVector:
 
     @staticmethod
     def zeros(size: int, L2: int = 128, device=None) -> "CiphertextVector":
-        """``CiphertextVector::zeros`` (lib.rs:434-437): literal 1 with exp 0 (:244-249)."""
+        """``CiphertextVector::zeros`` (lib.rs:434-437): literal 1 with exp 0 (:244-249).  As in
+        the reference it knows no key: a key-less (raw) vector of the integer 1, which the first
+        operation that supplies a key turns into M(1) (:func:`_resolve`)."""
         dev = _device(device)
         v = CiphertextVector.empty(size, L2, dev)
         v.C.zero_()
         v.C[:, 0, :] = 1
+        v.raw = True
         return v
 
     def to_signed_ints(self, ns: Optional[int] = None) -> Tuple[List[int], List[int]]:
         """Reference (signed rug::Integer, exp) pairs, for parity checks and the wire (ns may
         be omitted for a raw vector, or one whose signs are all 0)."""
+        if not self.raw:
+            n = self.n if self.n is not None else (_isqrt_exact(ns) if ns is not None else None)
+            if n is None:
+                raise TypeError("to_signed_ints: a keyed vector without its key")
+            mag, neg, exp = self.export_signed(PK(n))
+            mags = limbs_to_ints(mag.cpu().numpy().view(np.uint32))
+            sg = neg.cpu().numpy()
+            return [-m if s else m for m, s in zip(mags, sg)], exp.cpu().tolist()
         rows = tiles_to_rows(self.C.cpu().numpy().view(np.uint32), self.count)
         mags = limbs_to_ints(rows)
         sg = self.sign[: self.count].cpu().numpy()
-        if self.raw:
-            out = [-m if s else m for m, s in zip(mags, sg)]
-        else:
-            if ns is None and sg.any():
-                raise TypeError("to_signed_ints: negative elements need the key's n^2")
-            out = [m - ns if (s and m) else m for m, s in zip(mags, sg)]
-        return out, self.exp[: self.count].cpu().tolist()
+        return [-m if s else m for m, s in zip(mags, sg)], self.exp[: self.count].cpu().tolist()
 
     @staticmethod
     def from_signed_ints(cs: Sequence[int], exps: Sequence[int], ns: int, L2: int, device=None) -> "CiphertextVector":
+        """The reference's signed integers (|c| < n^2) under the key of modulus^2 ns, on the
+        device in the Montgomery-resident form (fphe_import_signed)."""
         dev = _device(device)
         count = len(cs)
-        canon = [c + ns if c < 0 else c for c in cs]
-        tiles = rows_to_tiles(ints_to_limbs(canon, L2))
+        tiles = rows_to_tiles(ints_to_limbs([abs(c) for c in cs], L2))
         C = torch.from_numpy(tiles.view(np.int32)).to(dev)
         sign = _pad_flat(torch.tensor([1 if c < 0 else 0 for c in cs], dtype=torch.uint8), count).to(dev)
         ex = _pad_flat(torch.tensor(list(exps), dtype=torch.int32), count).to(dev)
-        return CiphertextVector(C, sign, ex, count, _isqrt_exact(ns))
+        v = CiphertextVector(C, sign, ex, count, None, raw=True)
+        n = _isqrt_exact(ns)
+        if n is None:
+            raise ValueError("from_signed_ints: ns is not the square of a modulus")
+        _resolve(v, n)
+        return v
 
     def export_signed(self, pk: "PK") -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
         """The reference's signed integers on the device (fphe_export_signed): magnitudes as
@@ -525,13 +550,12 @@ class CiphertextVector:
     # ---- pickling: the reference's state, bincode(CiphertextVector) (paillier.rs:219-226) --
     def signed_rows(self) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
         """The reference's signed integers as (element-major magnitudes [count, L2], negative
-        flags, exps) on the device, from the key this vector carries (a raw vector, or one
-        with no negative element, needs none)."""
-        if self.raw or (self.n is None and not bool(self.sign[: self.count].any())):
+        flags, exps) on the device, from the key this vector carries (a raw vector needs none)."""
+        if self.raw:
             mag = tiles_to_cols(self.C).t()[: self.count].contiguous()
             return mag, self.sign[: self.count].contiguous(), self.exp[: self.count].clone()
         if self.n is None:
-            raise TypeError("CiphertextVector: negative elements and no key; build it through a PK operation "
+            raise TypeError("CiphertextVector: a keyed vector without its key; build it through a PK operation "
                             "before pickling")
         return self.export_signed(PK(self.n))
 
@@ -805,14 +829,15 @@ class CiphertextVector:
         folded, present = _fold_to_segments(pk, other, slot, self.count, index=src, with_present=True, deferred=errs)
         cur = _fit_limbs(self, pk._key.L2)
         r = _add(pk, cur, folded, broadcast=False)
+        if _fold_failed(errs):  # an exponent gap beyond the device merge: the exact torch path
+            folded, present = _fold_dense(pk, other, slot, self.count, src)
+            r = _add(pk, cur, folded, broadcast=False)
         # slots no term reaches keep their value as it was (exponent of a literal 1 included:
         # the reference never touches them)
         keep = present[: r.sign.numel()] == 0
         r.C = torch.where(keep.view(-1, 1, WAVE), cur.C, r.C)
         r.sign = torch.where(keep, cur.sign, r.sign)
         r.exp = torch.where(keep, cur.exp, r.exp)
-        for e in errs:
-            _fold_check(e)
         self.C, self.sign, self.exp = r.C, r.sign, r.exp
 
     def chunking_cumsum_with_step(self, pk: "PK", chunk_sizes: Sequence[int], step: int) -> None:
@@ -973,6 +998,46 @@ def _add_order(ea: torch.Tensor, eb: torch.Tensor, L2: int) -> Optional[torch.Te
     return order
 
 
+def _prealign(pk: "PK", a: CiphertextVector, b: CiphertextVector, n: int
+              ) -> Tuple[CiphertextVector, CiphertextVector]:
+    """Operands whose exponent gap exceeds MAX_GAP (the add kernel's exact range, kMaxGap):
+    the higher-exponent one, unless either is the literal 1 (add's identity, returned as it
+    is), is raised to 16^(gap - MAX_GAP) and its exponent lowered by as much, in fphe_align
+    steps of at most MAX_GAP -- decrese_exp_to (fixedpoint_paillier/src/lib.rs:250-258) split
+    into powers that compose: x^(16^(g1 + g2)) = (x^(16^g1))^(16^g2).  The add that follows
+    then has gaps <= MAX_GAP and returns the reference's integers.  Gaps beyond MAX_EXACT_GAP
+    (4 x 2^20 squarings per element) raise ValueError instead of running for hours.
+    Returns copies; the inputs are untouched."""
+    dev = a.device
+    gap = a.exp[:n].to(torch.int64) - b.exp[:n].to(torch.int64)
+    lit = _is_literal_one(pk, a)[:n] | _is_literal_one(pk, b)[:n]
+    big = (gap.abs() > MAX_GAP) & ~lit
+    idx = torch.nonzero(big).squeeze(1)
+    if idx.numel() == 0:
+        return a, b
+    g = gap[idx]
+    if int(g.abs().max()) > MAX_EXACT_GAP:
+        raise ValueError(f"exponent gap {int(g.abs().max())} beyond {MAX_EXACT_GAP} in ct-add "
+                         f"(4 squarings per step): corrupt exponents")
+    a, b = a.__copy__(), b.__copy__()
+    for side, sel in ((a, g > 0), (b, g < 0)):
+        sidx = idx[sel]
+        if sidx.numel() == 0:
+            continue
+        steps = g[sel].abs() - MAX_GAP
+        sub = side._gather(sidx)
+        rem = steps.clone()
+        while int(rem.max()) > 0:
+            st = rem.clamp(max=MAX_GAP)
+            e0 = sub.exp.clone()
+            sub = _align(pk, sub, st)
+            sub.exp.copy_(e0)
+            rem -= st
+        sub.exp[: sidx.numel()] -= steps.to(torch.int32)
+        side._assign(sidx.to(dev), sub)
+    return a, b
+
+
 def _add(pk: "PK", a: CiphertextVector, b: CiphertextVector, broadcast: bool, count: Optional[int] = None,
          reorder: bool = True) -> CiphertextVector:
     dev = a.device
@@ -983,6 +1048,12 @@ def _add(pk: "PK", a: CiphertextVector, b: CiphertextVector, broadcast: bool, co
     out = CiphertextVector.empty(n, a.L2, dev)
     if n == 0:
         return out
+    # the kernel is exact for exponent gaps up to MAX_GAP (one read-back of the largest gap)
+    eb = b.exp[:1].expand(n) if broadcast else b.exp[:n]
+    if int((a.exp[:n].to(torch.int64) - eb.to(torch.int64)).abs().max()) > MAX_GAP:
+        if broadcast:
+            b, broadcast = b._gather(torch.zeros(n, dtype=torch.long)), False
+        a, b = _prealign(pk, a, b, n)
     lib = _lib.load()
     ctx = pk._key.ctx(dev)
     stream = ctypes.c_void_p(_stream(dev))
@@ -996,7 +1067,7 @@ def _add(pk: "PK", a: CiphertextVector, b: CiphertextVector, broadcast: bool, co
         bC, bs, be = (b.C, b.sign, b.exp) if broadcast else (b.C[t0:t1], b.sign[e0:e1], b.exp[e0:e1])
         _lib.check(lib.fphe_add_ordered(ctx, _ptr(a.C[t0:t1]), _ptr(a.sign[e0:e1]), _ptr(a.exp[e0:e1]), _ptr(bC),
                                         _ptr(bs), _ptr(be), 0 if broadcast else 1, m, _ptr(order),
-                                        _ptr(out.C[t0:t1]), _ptr(out.sign[e0:e1]), _ptr(out.exp[e0:e1]), stream),
+                                        _ptr(out.C[t0:t1]), _ptr(out.sign[e0:e1]), _ptr(out.exp[e0:e1]), None, stream),
                    "fphe_add_ordered")
         del order  # the launch is stream-ordered: the allocator reuses the block only after it
     return out
@@ -1087,13 +1158,11 @@ def _fold_segments(pk: "PK", src: CiphertextVector, seg: torch.Tensor, index: Op
     cur, ckeys = _fold_chunks(pk, src, index[order], key)
     while bool((ckeys[1:] == ckeys[:-1]).any()):
         cur, ckeys = _fold_chunks(pk, cur, torch.arange(cur.count, device=dev), ckeys)
-    if MERGE_BY_ALIGN:
-        res, ids = _merge_exponents(pk, cur, ckeys)
-    else:
-        res, ids = _fold_tree(pk, cur, ckeys >> 32)
+    merged = _merge_exponents(pk, cur, ckeys) if MERGE_BY_ALIGN else None
+    res, ids = merged if merged is not None else _fold_tree(pk, cur, ckeys >> 32)
     # A segment whose terms are all the literal 1 folds to 1: add(1, y) returns y, so the
     # reference's sequential fold ends on its LAST term, exponent included (lib.rs:303-308).
-    lit = _is_literal_one(res)
+    lit = _is_literal_one(pk, res)
     if bool(lit.any()):
         pos = torch.arange(n, device=dev)
         last = torch.zeros(int(seg.max()) + 1, dtype=torch.long, device=dev)
@@ -1103,10 +1172,32 @@ def _fold_segments(pk: "PK", src: CiphertextVector, seg: torch.Tensor, index: Op
     return res, ids
 
 
-def _fold_check(err: torch.Tensor) -> None:
-    """Raise on the device error flags of a fold (reads them back: synchronises)."""
-    if int(err.item()) & _lib.EF_EXP_RANGE:
-        raise ValueError(f"exponent gap beyond {MAX_GAP} in a fold: corrupt exponents")
+def _fold_failed(errs: Sequence[torch.Tensor]) -> bool:
+    """Did a device fold meet an exponent gap beyond its exact range (FPHE_EF_EXP_RANGE)?
+    Reads the flags back (synchronises); the caller then folds with :func:`_fold_dense`."""
+    return any(int(e.item()) & _lib.EF_EXP_RANGE for e in errs)
+
+
+def _literal_ones(pk: "PK", count: int, dev) -> CiphertextVector:
+    """``count`` literal 1s (exp 0) under pk's key: M(1) words, sign 0."""
+    v = CiphertextVector.empty(count, pk._key.L2, dev)
+    v.C.copy_(pk._key.mont_one(dev).view(1, -1, 1).expand_as(v.C))
+    v.n = pk.n
+    return v
+
+
+def _fold_dense(pk: "PK", src: CiphertextVector, seg: torch.Tensor, nseg: int, idx: Optional[torch.Tensor]):
+    """out[s] for every s < nseg by the torch grouping of :func:`_fold_segments` (exact for any
+    exponent gap up to MAX_EXACT_GAP): the fallback of fphe_fold_segments for key spaces too
+    large for its counting sort and for gaps beyond its alignment range.  Returns (out, present)."""
+    dev = src.device
+    res, ids = _fold_segments(pk, src, seg.long(), index=None if idx is None else idx.long())
+    res.n = pk.n
+    out = _literal_ones(pk, nseg, dev)
+    out._assign(ids, res)
+    present = torch.zeros(_ntiles(nseg) * WAVE, dtype=torch.uint8, device=dev)
+    present[ids] = 1
+    return out, present
 
 
 def _fold_to_segments(pk: "PK", src: CiphertextVector, seg: torch.Tensor, nseg: int,
@@ -1117,7 +1208,8 @@ def _fold_to_segments(pk: "PK", src: CiphertextVector, seg: torch.Tensor, nseg: 
     :func:`_fold_segments` when the (segment, exponent) key space is too large for it.
     with_present: also return the per-segment uint8 flags "some term landed here".
     deferred: a list to append the device error flags to instead of reading them back here
-    (the caller then calls :func:`_fold_check` once its follow-up launches are queued)."""
+    (the caller then calls :func:`_fold_failed` once its follow-up launches are queued, and
+    folds with :func:`_fold_dense` if it reports a gap beyond the device merge's range)."""
     dev = src.device
     src = _fit_limbs(src, pk._key.L2)
     L2 = pk._key.L2
@@ -1138,26 +1230,23 @@ def _fold_to_segments(pk: "PK", src: CiphertextVector, seg: torch.Tensor, nseg: 
                                         _ptr(idx), _ptr(seg), T, nseg, _ptr(out.C), _ptr(out.sign), _ptr(out.exp),
                                         _ptr(present), _ptr(err), ctypes.c_void_p(_stream(dev)))
     if st == _lib.FPHE_ERR_RANGE:
-        res, ids = _fold_segments(pk, src, seg.long(), index=None if idx is None else idx.long())
-        out = CiphertextVector.zeros(nseg, L2, dev)
-        out._assign(ids, res)
-        out.n = pk.n
-        present[ids] = 1
+        out, present = _fold_dense(pk, src, seg, nseg, idx)
         return (out, present) if with_present else out
     if st == _lib.FPHE_ERR_ARG:
         raise PanicException("index out of bounds")
     _lib.check(st, "fphe_fold_segments")
     if deferred is not None:
         deferred.append(err)
-    else:
-        _fold_check(err)
+    elif _fold_failed([err]):
+        out, present = _fold_dense(pk, src, seg, nseg, idx)
     return (out, present) if with_present else out
 
 
-def _is_literal_one(v: CiphertextVector) -> torch.Tensor:
-    """Per element: is the signed ciphertext integer exactly 1 (the reference's zero)."""
-    C = v.C
-    lit = ((C[:, 0, :] == 1) & (C[:, 1:, :] == 0).all(dim=1)).reshape(-1)[: v.count]
+def _is_literal_one(pk: "PK", v: CiphertextVector) -> torch.Tensor:
+    """Per element: is the signed ciphertext integer exactly 1 (the reference's zero), i.e. is
+    C = M(1) with sign 0 (Montgomery-resident words)."""
+    one = pk._key.mont_one(v.device).view(1, -1, 1)
+    lit = (v.C == one).all(dim=1).reshape(-1)[: v.count]
     return lit & (v.sign[: v.count] == 0)
 
 
@@ -1165,10 +1254,13 @@ def _is_literal_one(v: CiphertextVector) -> torch.Tensor:
 # the pairwise ct-add tree (False: ceil(log2(partials)) launches, each as long as its largest
 # exponent gap)
 MERGE_BY_ALIGN = True
-MAX_GAP = 1 << 16  # kMaxGap of fate_amd/csrc/kernels27.h
+MAX_GAP = 1 << 16  # kMaxGap of fate_amd/csrc/kernels27.h: the add / align kernels' exact range
+# larger gaps are split into fphe_align steps (_prealign) up to this many, else ValueError
+MAX_EXACT_GAP = 1 << 20
 
 
-def _merge_exponents(pk: "PK", cur: CiphertextVector, ckeys: torch.Tensor) -> Tuple[CiphertextVector, torch.Tensor]:
+def _merge_exponents(pk: "PK", cur: CiphertextVector, ckeys: torch.Tensor
+                     ) -> Optional[Tuple[CiphertextVector, torch.Tensor]]:
     """One ciphertext per segment from its per-exponent partials (keys (segment << 32) |
     (exp + 2^31), ascending, one partial per key).  The reference's sequential adds raise
     every term to 16^(e - e_min), e_min the least exponent of the segment's non-literal
@@ -1183,15 +1275,15 @@ def _merge_exponents(pk: "PK", cur: CiphertextVector, ckeys: torch.Tensor) -> Tu
     n = cur.count
     seg = ckeys >> 32
     exp = (ckeys & 0xFFFFFFFF) - (1 << 31)
-    lit = _is_literal_one(cur)
+    lit = _is_literal_one(pk, cur)
     big = 1 << 40
     _, inv = torch.unique_consecutive(seg, return_inverse=True)
     emin = torch.full((int(inv.max()) + 1,), big, dtype=torch.long, device=dev)
     emin.scatter_reduce_(0, inv, torch.where(lit, torch.full_like(exp, big), exp), reduce="amin")
     em = emin[inv]
     gap = torch.where(lit | (em == big), torch.zeros_like(exp), exp - em)
-    if int(gap.max()) > MAX_GAP:  # fphe_align's contract (kMaxGap in kernels27.h)
-        raise ValueError(f"exponent gap beyond {MAX_GAP} (4 x {MAX_GAP} squarings per term): corrupt exponents")
+    if int(gap.max()) > MAX_GAP:  # fphe_align's contract (kMaxGap in kernels27.h): the caller
+        return None               # merges by the pairwise ct-add tree, exact for such gaps
     tgt = torch.where(em == big, torch.zeros_like(em), em)
     order = torch.argsort(gap, descending=True, stable=True)
     src = cur._gather(order)
@@ -1643,13 +1735,11 @@ class Evaluator:
     @staticmethod
     def cat(vec_list: Sequence[CiphertextVector]) -> CiphertextVector:
         n = next((v.n for v in vec_list if v.n is not None), None)
-        if n is not None:  # key-less unpickled parts join a keyed vector under its key
+        if n is not None:  # key-less parts (unpickled, zeros()) join a keyed vector under its key
             _resolve_args(n, list(vec_list))
         elif any(v.raw for v in vec_list) and not all(v.raw for v in vec_list if v.count):
-            # raw parts beside key-less keyed parts (e.g. zeros()): only sign-0 parts can go raw
-            for v in vec_list:
-                if not v.raw and bool(v.sign[: v.count].any()):
-                    raise TypeError("cat of an unpickled (key-less) vector with a vector of unknown key")
+            # Montgomery-resident words of an unknown key cannot join signed integers
+            raise TypeError("cat of a key-less vector with a vector of unknown key")
         out = Evaluator._cat(vec_list)
         out.n = n
         out.raw = n is None and any(v.raw for v in vec_list if v.count)

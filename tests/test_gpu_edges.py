@@ -386,12 +386,11 @@ def test_extreme_operands(bits):
         assert host(enc) == [(c.c, c.exp) for c in want]
 
 
-def _rows(v, idx):
-    """(signed integer, exp) of elements idx of a device vector, read without a full copy."""
+def _rows(v, idx, pk):
+    """The reference's (signed integer, exp) of elements idx of a device vector, read without
+    a full copy (the elements are gathered, then exported out of the Montgomery form)."""
     idx_t = torch.as_tensor(idx, dtype=torch.long, device=v.C.device)
-    words = v.C[idx_t // 64, :, idx_t % 64].cpu().numpy().view(np.uint32)
-    mags = [sum(int(w) << (32 * k) for k, w in enumerate(row)) for row in words]
-    return mags, v.sign[idx_t].cpu().tolist(), v.exp[idx_t].cpu().tolist()
+    return v._gather(idx_t).to_signed_ints(pk.ns)
 
 
 def test_add_across_launch_chunks():
@@ -417,28 +416,23 @@ def test_add_across_launch_chunks():
     a, b = rand_vec(), rand_vec()
     seam = P.ADD_CHUNK
     lits = [0, seam - 1, seam, n - 1]
+    one = pk._key.mont_one(dev)  # the literal 1 as stored: M(1)
     for i in lits[:2]:  # literal 1s on both sides of the seam
-        a.C[i // 64, :, i % 64] = 0
-        a.C[i // 64, 0, i % 64] = 1
+        a.C[i // 64, :, i % 64] = one
         a.sign[i] = 0
     for i in lits[2:]:
-        b.C[i // 64, :, i % 64] = 0
-        b.C[i // 64, 0, i % 64] = 1
+        b.C[i // 64, :, i % 64] = one
         b.sign[i] = 0
     out = a.add(pk, b)
     rng = random.Random(9)
     idx = sorted(set(lits + [1, 63, 64, seam - 64, seam - 2, seam + 1, seam + 63, seam + 64, n - 2, n - 64]
                      + [rng.randrange(n) for _ in range(24)]))
-    ma, sa, ea = _rows(a, idx)
-    mb, sb, eb = _rows(b, idx)
-    mo, so, eo = _rows(out, idx)
-    ns = opk.ns
+    (ca, ea), (cb, eb), (co, eo) = _rows(a, idx, pk), _rows(b, idx, pk), _rows(out, idx, pk)
+    for k in lits:
+        assert ca[idx.index(k)] == 1 or cb[idx.index(k)] == 1, k  # M(1) is the integer 1
     for k in range(len(idx)):
-        ca = O.Ciphertext(ma[k] - ns if sa[k] and ma[k] else ma[k], ea[k])
-        cb = O.Ciphertext(mb[k] - ns if sb[k] and mb[k] else mb[k], eb[k])
-        want = O.ct_add(opk, ca, cb)
-        got = mo[k] - ns if so[k] and mo[k] else mo[k]
-        assert (got, eo[k]) == (want.c, want.exp), idx[k]
+        want = O.ct_add(opk, O.Ciphertext(ca[k], ea[k]), O.Ciphertext(cb[k], eb[k]))
+        assert (co[k], eo[k]) == (want.c, want.exp), idx[k]
 
 
 @pytest.mark.parametrize("keyholder", [False, True], ids=["public", "keyholder_crt"])

@@ -76,7 +76,8 @@ def test_fold_segments_many_levels_and_torch_grouping(env):
     seg = torch.randint(0, 5, (T,), generator=g)
     got = P._fold_to_segments(pk, v, seg, 6, index=idx)
     res, ids = P._fold_segments(pk, v, seg, index=idx)
-    want = P.CiphertextVector.zeros(6, pk._key.L2)
+    want = P._literal_ones(pk, 6, v.device)
+    res.n = pk.n
     want._assign(ids, res)
     assert host(pk, got) == host(pk, want)
     # and segment 0 against the oracle (a strided subset of its terms keeps this quick)

@@ -404,5 +404,5 @@ def test_neg_batch_inversion_full_grid(env):
     a = pk.encrypt_encoded(coder.encode_f32_vec(x), True)
     prod = P._add(pk, a, P._neg(pk, a), False)
     C = prod.C.transpose(1, 2).reshape(-1, prod.L2)[:n]  # tile-major [tiles][L2][64] -> rows
-    assert bool((C[:, 0] == 1).all()) and bool((C[:, 1:] == 0).all())
+    assert bool((C == pk._key.mont_one(C.device)).all())  # M(1): the integer 1 in Montgomery form
     assert torch.equal(prod.exp[:n], a.exp[:n])
