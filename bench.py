@@ -148,13 +148,15 @@ def pmc_traffic_per_elem():
 
 
 def pmc_ops_traffic(op: str):
-    """HBM bytes per element of the decrypt ("decrypt") or ct-add ("ct_add") kernels from the
-    committed PMC passes (tools/pmc_ops_summary.py), or (None, None)."""
+    """HBM bytes per element of the decrypt / ct_add / ct_mul kernels (per term for iupdate)
+    from the committed PMC passes (tools/pmc_ops_summary.py), or (None, None)."""
     path = _pmc_profile("ops", "*pmc_ops.json")
     if not path:
         return None, None
     with open(path) as f:
         d = json.load(f)
+    if op not in d:
+        return None, None
     return float(d[op]["hbm_bytes_per_elem"]), os.path.relpath(path, ROOT)
 
 
@@ -190,6 +192,8 @@ def cpu_baseline(p: int, q: int, seconds: float = 3.0):
         "decrypt_per_s": ops["decrypt"]["per_s"],
         "ct_add_per_s": ops["add"]["per_s"],
         "ct_add_hetero_lr_gaps_per_s": ops["add_gap"]["per_s"],
+        "ct_mul_per_s": ops["mul"]["per_s"],
+        "iupdate_per_s": ops["iupdate"]["per_s"],
         "cpu_model": d["cpu_model"],
         "machine_cores": d["machine_cores"],
         "usable_cores": d["usable_cores"],
@@ -206,17 +210,36 @@ def cpu_baseline(p: int, q: int, seconds: float = 3.0):
                    f"reference's call order (oracle/gmp_ref.c), 2048-bit key: {ops['encrypt']['elements']} "
                    f"obfuscated encryptions, {ops['decrypt']['elements']} CRT decryptions, "
                    f"{ops['add']['elements']} aligned ct-adds (mpz_mul + tdiv_r), {ops['add_gap']['elements']} ct-adds "
-                   f"with the Hetero-LR exponent-gap mix (+ mpz_powm by 16^gap)"),
+                   f"with the Hetero-LR exponent-gap mix (+ mpz_powm by 16^gap), {ops['mul']['elements']} ct x pt "
+                   f"by float32 weights in [-1, 2) (mpz_powm by the significand, mpz_invert first for a third), "
+                   f"{ops['iupdate']['elements']} iupdate scatter-adds of SecureBoost-shaped g, h terms into 256 "
+                   f"slots (sequential Ciphertext::add with decrese_exp_to)"),
     }
 
 
-def valu_roofline(kernel: str, mac32: float, ms: float, hbm_bytes: float, **extra) -> dict:
+def hbm_block(alg_bytes: float, ms: float, traffic=None, source=None) -> dict:
+    """HBM view of one timed launch: the algorithmic bytes' rate and, when the committed
+    rocprofv3 FETCH_SIZE / WRITE_SIZE passes cover the kernel (`traffic`, bytes per launch at
+    this size), the counter bytes' rate (hbm_counter_GBps, north_star's "achieved HBM GB/s from
+    rocprof") and their ratio to the algorithmic bytes (re-reads and spills)."""
+    sec = ms / 1e3
+    out = {"achieved": round(alg_bytes / sec / 1e9, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+           "algorithmic_bytes": round(alg_bytes)}
+    if traffic is not None:
+        out.update({"counter_bytes": round(traffic), "hbm_counter_GBps": round(traffic / sec / 1e9, 3),
+                    "counter_frac_of_peak": round(traffic / sec / 1e9 / PEAK_HBM_GBS, 4),
+                    "counter_over_algorithmic": round(traffic / alg_bytes, 2), "counter_source": source})
+    return out
+
+
+def valu_roofline(kernel: str, mac32: float, ms: float, hbm_bytes: float, traffic=None, traffic_source=None,
+                  **extra) -> dict:
     """A roofline block in SURVEY.md §8(d)'s MAC32 accounting for one timed launch."""
     achieved = mac32 / (ms / 1e3) / 1e12
     return {"bound": "valu", "kernel": kernel, "achieved": round(achieved, 3), "peak": round(PEAK_TMAC32, 3),
             "unit": "TMAC32/s", "frac": round(achieved / PEAK_TMAC32, 4), "kernel_ms": round(ms, 3),
-            "hbm": {"achieved": round(hbm_bytes / (ms / 1e3) / 1e9, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s"},
-            **extra}
+            "traffic": None if traffic is None else round(traffic), "traffic_source": traffic_source,
+            "hbm": hbm_block(hbm_bytes, ms, traffic, traffic_source), **extra}
 
 
 def add_kernel_leg(P, pk, a, b, N, stream, dev) -> dict:
@@ -266,6 +289,7 @@ def add_kernel_leg(P, pk, a, b, N, stream, dev) -> dict:
     wave_sq = 4 * gs.view(-1, per_wave).amax(1).double().sum().item() * per_wave
     mads = N * 2 * NL * NL + wave_sq * NL * TPI * (ENGINE_LL // 2 + 1 + ENGINE_LL)
     blk = valu_roofline("k_add27<128> (exponent-gap order)", mac, ms, N * (3 * (L * 4 + 5) + 4),
+                        traffic=_traffic("ct_add", N), traffic_source=pmc_ops_traffic("ct_add")[1],
                         per_elem_mac32=round(mac / N, 1), gap_histogram=hist, sorted=order is not None)
     blk["issue"] = {"mad64_per_elem": round(mads / N, 1), "achieved": round(mads / (ms / 1e3) / 1e12, 3),
                     "peak": round(PEAK_TMAC32, 3), "unit": "Tmad/s",
@@ -298,8 +322,12 @@ def iupdate_roofline(src, positions, stride: int, nslots: int, seconds: float, k
     terms = int(slot.numel())
     L = key_bits // 16
     mac = (terms + align_sq) * mac32_per_mont(L)
-    blk = valu_roofline("fphe_fold_segments (k_gr_* grouping, k_fold27 levels, k_align_rows27) + k_add27",
+    # counter bytes: the fold's row copy and balanced level (the bulk of the call's traffic),
+    # per term from the committed PMC passes, over the whole call's time
+    blk = valu_roofline("fphe_fold_segments (k_gr_* grouping, k_segfold27 + k_fold27 levels, k_align_rows27) + k_add27",
                         mac, seconds * 1e3, terms * (key_bits // 4 + 5) + nslots * 3 * (key_bits // 4 + 5),
+                        traffic=_traffic("iupdate", terms) if key_bits == 2048 else None,
+                        traffic_source=pmc_ops_traffic("iupdate")[1],
                         per_term_mac32=round(mac / terms, 1), terms=terms, slots=nslots,
                         alignment_squarings=align_sq, scope="end to end (the whole iupdate call)")
     blk["scatter_adds_per_s"] = round(terms / seconds, 1)
@@ -428,6 +456,8 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip decrypt/add/e2e legs")
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the ciphertext all-gather leg")
+    ap.add_argument("--config4-samples", type=int, default=10_000_000,
+                    help="BASELINE config 4 leg (histogram_config4): samples in all, split over the ranks; 0 skips it")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -517,7 +547,20 @@ def main() -> None:
     # sits on each rank as the federation sender needs it.  Reported beside `value`.
     gather_info = {}
     if dist and not args.no_gather:
-        from fate_amd.dist import gather_tiles
+        from fate_amd.dist import gather_tiles, gather_tiles_to
+        # onto rank 0 only (the federation sender: fate_amd.dist.gather_tiles_to, point to
+        # point), then onto every rank (the all-gather)
+        barrier()
+        tg = time.perf_counter()
+        got = gather_tiles_to(ct.C, ct.sign, ct.exp, ct.count, 0, trim=False)
+        barrier()
+        g1 = time.perf_counter() - tg
+        tt = torch.tensor([g1], dtype=torch.float64, device=dev)
+        tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
+        g1 = float(tt.item())
+        total0 = sum(got[3]) if got is not None else 0
+        del got
+        torch.cuda.empty_cache()
         barrier()
         tg = time.perf_counter()
         Cg, sg, eg, counts = gather_tiles(ct.C, ct.sign, ct.exp, ct.count, trim=False)
@@ -535,6 +578,10 @@ def main() -> None:
                           "recv_GBps_per_rank": round(recv / gs / 1e9, 2),
                           "encrypt_plus_allgather_per_s": round((args.total if strong else world * N)
                                                                 / (elapsed / args.steps + gs), 1)},
+            "gather_to_rank0": {"seconds": round(g1, 4), "elements": int(total0),
+                                "recv_GBps_rank0": round((total0 - ct.count) * per_elem / g1 / 1e9, 2),
+                                "encrypt_plus_gather_per_s": round((args.total if strong else world * N)
+                                                                   / (elapsed / args.steps + g1), 1)},
         }
         del Cg, sg, eg
 
@@ -767,17 +814,30 @@ def main() -> None:
                                          N * (key_bits // 4 + 4 + key_bits // 8),
                                          traffic=_traffic("decrypt", N), traffic_source=pmc_ops_traffic("decrypt")[1]),
                 "iupdate": iupdate_block,
-                "ct_add": dict(add_kernel, traffic=_traffic("ct_add", N),
-                               traffic_source=pmc_ops_traffic("ct_add")[1]),
+                "ct_add": add_kernel,
                 # §8(d): float significands (E = 56): (56 + 12 + 16) mulmods over L = 128, + 3
                 # for each negative weight (the inverse branch); the whole op is timed:
                 # classify, batch inverse of the negative-weight elements, the powm
                 "ct_mul": valu_roofline("k_mul_prep + k_binv_pre27/k_inv_n27/k_inv_lift27/k_binv_post27 + k_mul27<128,4>",
                                         (N * (56 + 12 + 16) + 3 * n_neg) * mac32_per_mont(key_bits // 16), mul_ms,
-                                        N * 2 * (key_bits // 4 + 5) + N * 13, negative_weights=n_neg),
+                                        N * 2 * (key_bits // 4 + 5) + N * 13, traffic=_traffic("ct_mul", N),
+                                        traffic_source=pmc_ops_traffic("ct_mul")[1], negative_weights=n_neg),
             },
         }
         del pt, y, ct2, s, ce, Ch, m, gh, hist
+        # BASELINE config 4 at its stated size (10M samples x 10 features x 32 bins, 2048-bit):
+        # unpacked ct x pt + the 200M-term iupdate, packed iupdate + cumsum + squeeze, sharded
+        # over the ranks with the cross-rank fold (tools/bench_legs/secureboost_full.py)
+        if args.config4_samples > 0:
+            import importlib.util
+            spec = importlib.util.spec_from_file_location(
+                "secureboost_full", os.path.join(ROOT, "tools", "bench_legs", "secureboost_full.py"))
+            sbf = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(sbf)
+            torch.cuda.empty_cache()
+            extras["histogram_config4"] = sbf.config4(P, pk_kh, sk, coder, dev, total=args.config4_samples, rank=rank,
+                                                      world=world, iupdate_roofline=iupdate_roofline)
+            torch.cuda.empty_cache()
 
     if rank != 0:
         if dist:
@@ -808,7 +868,7 @@ def main() -> None:
         # v_mad_u64_u32 each) against the same half-rate mad peak
         "issue": {"mad64_per_elem": enc_mad27_per_elem(key_bits, pk.n), "achieved": round(mad27, 3),
                   "peak": round(PEAK_TMAC32, 3), "unit": "Tmad/s", "frac": round(mad27 / PEAK_TMAC32, 4)},
-        "hbm": {"achieved": round(hbm_bytes / (enc_kernel_ms / 1e3) / 1e9, 3), "peak": PEAK_HBM_GBS, "unit": "GB/s"},
+        "hbm": hbm_block(hbm_bytes, enc_kernel_ms, round(tb * N) if tb is not None else None, tsrc),
     }
     out = {
         "metric": "Paillier-2048 encrypts/sec device-resident",
@@ -843,12 +903,16 @@ def main() -> None:
             ratios = {"encrypt_vs_pool": value / cb["value"], "encrypt_vs_1_process": value / sp["encrypt"],
                       "encrypt_vs_host_projection": value / hp if hp else None}
             if extras:
-                ratios.update({"decrypt_vs_pool": extras["decrypt_per_s"] / cb["decrypt_per_s"],
-                               "ct_add_hetero_lr_vs_pool": extras["ct_add_per_s"] / cb["ct_add_hetero_lr_gaps_per_s"],
-                               "decrypt_vs_host_projection": extras["decrypt_per_s"] / (cb["decrypt_per_s"] * hp
-                                                                                         / cb["value"]),
-                               "ct_add_hetero_lr_vs_host_projection": extras["ct_add_per_s"] / (
-                                   cb["ct_add_hetero_lr_gaps_per_s"] * hp / cb["value"])})
+                # the host projection scales every op's pool rate by the encrypt projection's
+                # host/pool factor (cores x SMT uplift)
+                host = hp / cb["value"]
+                gpu = {"decrypt": extras["decrypt_per_s"], "ct_add_hetero_lr": extras["ct_add_per_s"],
+                       "ct_mul": extras["ct_mul_per_s"], "iupdate": extras["histogram_scatter_adds_per_s"]}
+                cpu = {"decrypt": cb["decrypt_per_s"], "ct_add_hetero_lr": cb["ct_add_hetero_lr_gaps_per_s"],
+                       "ct_mul": cb["ct_mul_per_s"], "iupdate": cb["iupdate_per_s"]}
+                for k in gpu:
+                    ratios[f"{k}_vs_pool"] = gpu[k] / cpu[k]
+                    ratios[f"{k}_vs_host_projection"] = gpu[k] / (cpu[k] * host)
             cb["gpu_over_cpu"] = {k: (round(v, 2) if v is not None else None) for k, v in ratios.items()}
             out["cpu_baseline"] = cb
         except Exception as exc:  # GMP missing on the box: say so, do not fake a number

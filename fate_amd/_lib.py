@@ -68,8 +68,9 @@ def load() -> ctypes.CDLL:
         lib.fphe_ctx_destroy.restype = st
         lib.fphe_ctx_limbs.argtypes = [vp, c_u32p, c_u32p]
         lib.fphe_ctx_limbs.restype = st
-        lib.fphe_ctx_mont_one.argtypes = [vp, c_u32p]
-        lib.fphe_ctx_mont_one.restype = st
+        if hasattr(lib, "fphe_ctx_mont_one"):  # an A/B build from before it (FPHE_LIB_PATH) lacks it
+            lib.fphe_ctx_mont_one.argtypes = [vp, c_u32p]
+            lib.fphe_ctx_mont_one.restype = st
         for name in ("fphe_encode_f32", "fphe_encode_f64"):
             f = getattr(lib, name)
             f.argtypes = [vp, vp, ctypes.c_size_t, vp, vp, vp, vp, vp]

@@ -619,6 +619,18 @@ int bpc_for_slot(int slot_limbs) {
 namespace {
 // ---- reduced-radix engine launchers (kernels27.h) ---------------------------------------
 template <int L>
+fphe_status launch_mont_const27(fphe_ctx* c, const uint32_t* C, size_t count, const u32* X, uint32_t* Co,
+                                hipStream_t s) {
+  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = rad_ll(TPI) * TPI;
+  auto kern = KS<TPI>::template mont_const<L>();
+  const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
+  set_lds(kern, lds);
+  const unsigned grid = occ_grid(c, kern, lds, (count + E - 1) / E, "mont_const27");
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, C, count, X, Co, (u32)NL);
+  return hip_ok(hipGetLastError());
+}
+
+template <int L>
 fphe_status launch_encrypt27(fphe_ctx* c, const uint32_t* P, uint32_t lp, const uint8_t* neg, size_t count, int obf,
                              const uint32_t* r, const uint32_t key[8], uint64_t nonce, uint32_t* C, uint8_t* sign,
                              hipStream_t s) {
@@ -647,7 +659,9 @@ fphe_status launch_encrypt27(fphe_ctx* c, const uint32_t* P, uint32_t lp, const 
     }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, P + t0 * lp * FPHE_WAVE, lp, neg + e0, m, obf,
                        rbuf, C + t0 * L * FPHE_WAVE, sign + e0, c->scratch, (u32)LDSW);
-    if (hipGetLastError() != hipSuccess) return FPHE_ERR_HIP;
+    // into the Montgomery-resident form, in place (one product per element)
+    if (launch_mont_const27<L>(c, C + t0 * L * FPHE_WAVE, m, c->K.N2R2_27, C + t0 * L * FPHE_WAVE, s) != FPHE_OK)
+      return FPHE_ERR_HIP;
   }
   return FPHE_OK;
 }
@@ -1154,18 +1168,6 @@ fphe_status launch_sqmul27(fphe_ctx* c, const uint32_t* Ca, const uint32_t* Cb, 
   set_lds(kern, lds);
   const unsigned grid = occ_grid(c, kern, lds, (count + E - 1) / E, "sqmul27");
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, Ca, Cb, sb, nsq, count, Co, so, (u32)NL);
-  return hip_ok(hipGetLastError());
-}
-
-template <int L>
-fphe_status launch_mont_const27(fphe_ctx* c, const uint32_t* C, size_t count, const u32* X, uint32_t* Co,
-                                hipStream_t s) {
-  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = rad_ll(TPI) * TPI;
-  auto kern = KS<TPI>::template mont_const<L>();
-  const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
-  set_lds(kern, lds);
-  const unsigned grid = occ_grid(c, kern, lds, (count + E - 1) / E, "mont_const27");
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, C, count, X, Co, (u32)NL);
   return hip_ok(hipGetLastError());
 }
 

@@ -4,10 +4,11 @@ Paillier encrypt / decrypt / ct-add / ct x pt are independent per element, so a 
 ``count`` elements is split into contiguous, tile-aligned (64-element) ranges, one per rank
 -- the same decomposition as the reference's ``DTensor.map_shard``
 (python/fate/arch/tensor/distributed/_tensor.py:365-385), with GPUs instead of computing
-partitions.  The only exchange step is the optional all-gather of the ciphertext shards
-when the consumer needs the whole vector in one place (e.g. the federation sender on rank
-0): one ``all_gather_into_tensor`` of the byte-packed tiles per component, over RCCL/xGMI
-on GPUs (backend "nccl") or gloo on CPU.  Reductions across ranks are gather-then-modmul
+partitions.  The only exchange step is the optional gather of the ciphertext shards when
+the consumer needs the whole vector in one place: onto one rank (the federation sender,
+:func:`gather_tiles_to`, point-to-point) or onto every rank (:func:`gather_tiles`, one
+``all_gather_into_tensor`` of the byte-packed tiles per component), over RCCL/xGMI on GPUs
+(backend "nccl") or gloo on CPU.  Reductions across ranks are gather-then-modmul
 (RCCL has no modular-product reduce), as the reference's ``map_reduce_shard(..., add)``
 (_tensor.py:387-395) reduces per-partition partials; ciphertext folds are order independent
 (SURVEY.md §0 fact 3), so that stays bit-exact.
@@ -112,12 +113,74 @@ def gather_tiles(C: torch.Tensor, sign: torch.Tensor, exp: torch.Tensor, count: 
     return compact_gathered(Cg, sg, eg, counts)
 
 
-def gather_ciphertexts(cv, group=None):
-    """All-gather a sharded ``fate_amd.paillier.CiphertextVector`` (every shard but the last
-    must be whole tiles, as produced by :func:`shard_bounds`).  The key stamp travels."""
+def gather_tiles_to(C: torch.Tensor, sign: torch.Tensor, exp: torch.Tensor, count: int, dst: int = 0, group=None,
+                    trim: bool = True):
+    """Gather the per-rank shards onto rank ``dst`` only -- the federation sender's case
+    (one party process sends the whole ciphertext vector), where an
+    all-gather would put every rank's copy of the vector in every GPU's HBM (52 GB per rank for
+    BASELINE config 5's 100M elements at 2048 bits).  Point-to-point over RCCL/xGMI: each other
+    rank sends its padded shard's three components, rank ``dst`` receives them straight into
+    one buffer (rank r's shard at tiles [r * nt_max, ...)) and compacts it as
+    :func:`gather_tiles` does.  The shard counts travel in one small all-gather first.  Returns
+    (C, sign, exp, total) on ``dst`` (with ``trim=False`` the padded buffers and the per-rank
+    counts) and None on every other rank."""
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = C.device
+    cnt = torch.tensor([count], dtype=torch.int64, device=dev)
+    counts = [torch.zeros_like(cnt) for _ in range(world)]
+    dist.all_gather(counts, cnt, group=group)
+    counts = [int(c.item()) for c in counts]
+    nt_max = max((c + WAVE - 1) // WAVE for c in counts) if counts else 0
+    L = C.shape[1]
+    mine = (_pad_tiles(C, nt_max), _pad_flat(sign.to(torch.uint8), nt_max * WAVE), _pad_flat(exp, nt_max * WAVE))
+    # gloo's point-to-point takes host tensors only (the CPU tests, and bench.py's gloo
+    # rehearsal of several ranks on one GPU); RCCL moves the device buffers directly
+    host = dist.get_backend(group) == "gloo"
+    if host:
+        mine = tuple(t.cpu() for t in mine)
+    if rank != dst:
+        for t in mine:
+            dist.send(t, dst, group=group)
+        return None
+    bdev = torch.device("cpu") if host else dev
+    Cg = torch.empty((world * nt_max, L, WAVE), dtype=C.dtype, device=bdev)
+    sg = torch.empty(world * nt_max * WAVE, dtype=torch.uint8, device=bdev)
+    eg = torch.empty(world * nt_max * WAVE, dtype=exp.dtype, device=bdev)
+    outs = (Cg, sg, eg)
+    per = (nt_max, nt_max * WAVE, nt_max * WAVE)
+    reqs = []
+    for r in range(world):
+        for buf, k, t in zip(outs, per, mine):
+            view = buf[r * k:(r + 1) * k]
+            if r == rank:
+                view.copy_(t)
+            else:
+                reqs.append(dist.irecv(view, r, group=group))
+    for q in reqs:
+        q.wait()
+    if host:
+        Cg, sg, eg = Cg.to(dev), sg.to(dev), eg.to(dev)
+    if not trim:
+        return Cg, sg, eg, counts
+    return compact_gathered(Cg, sg, eg, counts)
+
+
+def gather_ciphertexts(cv, group=None, dst=None):
+    """Gather a sharded ``fate_amd.paillier.CiphertextVector`` (every shard but the last must be
+    whole tiles, as produced by :func:`shard_bounds`): onto every rank (``dst`` None: the
+    all-gather) or onto rank ``dst`` only (None returned elsewhere).  The key stamp travels."""
     from .paillier import CiphertextVector
 
-    C, s, e, n = gather_tiles(cv.C, cv.sign, cv.exp, cv.count, group)
+    if dst is None:
+        C, s, e, n = gather_tiles(cv.C, cv.sign, cv.exp, cv.count, group)
+    else:
+        got = gather_tiles_to(cv.C, cv.sign, cv.exp, cv.count, dst, group)
+        if got is None:
+            return None
+        C, s, e, n = got
     return CiphertextVector(C, s, e, n, cv.n, cv.raw)
 
 

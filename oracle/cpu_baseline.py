@@ -2,7 +2,8 @@
 
 Times the libgmp restatement of the reference's per-element call sequence
 (oracle/gmp_ref.c: encrypt = crates/paillier/src/lib.rs:104-121, decrypt = :163-176,
-ct-add = :35-37) the way FATE runs it: one worker PROCESS per core, each a serial
+ct-add = :35-37, ct x pt = fixedpoint_paillier/src/lib.rs:334-349, the iupdate scatter-add =
+:724-735) the way FATE runs it: one worker PROCESS per core, each a serial
 element loop (the reference's Rust call is single-threaded, and FATE parallelises by a
 process pool of os.cpu_count() workers, arch/computing/backends/standalone/
 _standalone.py:470-478 and _csession.py:41-42).
@@ -37,9 +38,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 if os.path.dirname(HERE) not in sys.path:
     sys.path.insert(0, os.path.dirname(HERE))
 
-OPS = ("encrypt", "decrypt", "add", "add_gap")
+OPS = ("encrypt", "decrypt", "add", "add_gap", "mul", "iupdate")
 # elements of the short serial calibration run per op
-CALIB = {"encrypt": 20, "decrypt": 60, "add": 20000, "add_gap": 4000}
+CALIB = {"encrypt": 20, "decrypt": 60, "add": 20000, "add_gap": 4000, "mul": 200, "iupdate": 10000}
 
 
 def cpu_model() -> str:

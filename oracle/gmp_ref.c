@@ -10,6 +10,10 @@
  *   decrypt  crates/paillier/src/lib.rs:163-176  (2x h_function: powm, sub 1, tdiv_q,
  *            mul, tdiv_r; CRT with tdiv_r; +n if negative)
  *   add      crates/paillier/src/lib.rs:35-37    (mpz_mul + mpz_tdiv_r)
+ *   ct x pt  fixedpoint_paillier/src/lib.rs:334-349 (mpz_powm by the significand; a
+ *            negative one inverts the base first, mpz_invert, as GMP's powm does)
+ *   iupdate  fixedpoint_paillier/src/lib.rs:724-735 (a sequential Ciphertext::add of each
+ *            term into its slot, :301-333, decrese_exp_to's mpz_powm by 16^gap included)
  * The image ships libgmp.so.10 (6.2.1) without gmp.h, so the few entry points used are
  * declared below against GMP's documented, stable ABI (__gmpz_* symbols, mpz_t layout).
  */
@@ -17,6 +21,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <math.h>
 #include <time.h>
 
 typedef unsigned long mp_limb_t;
@@ -41,6 +46,7 @@ extern void __gmpz_tdiv_r(mpz_struct*, const mpz_struct*, const mpz_struct*);
 extern void __gmpz_tdiv_q(mpz_struct*, const mpz_struct*, const mpz_struct*);
 extern int __gmpz_invert(mpz_struct*, const mpz_struct*, const mpz_struct*);
 extern void __gmpz_urandomm(mpz_struct*, randstate_struct*, const mpz_struct*);
+extern void __gmpz_mul_2exp(mpz_struct*, const mpz_struct*, unsigned long);
 extern void __gmp_randinit_default(randstate_struct*);
 extern void __gmp_randseed_ui(randstate_struct*, unsigned long);
 extern void __gmp_randclear(randstate_struct*);
@@ -193,9 +199,55 @@ typedef struct {
   gref_ctx* c;
   long count;
   unsigned long seed;
-  int op;  /* 0 encrypt(obfuscated), 1 decrypt, 2 add (aligned), 3 add (Hetero-LR exponent gaps) */
+  int op;  /* 0 encrypt(obfuscated), 1 decrypt, 2 add (aligned), 3 add (Hetero-LR exponent gaps),
+              4 ct x pt (float32 weights in [-1, 2)), 5 iupdate (SecureBoost-shaped g, h terms) */
   double secs;
 } job_t;
+
+/* xorshift64* and a standard normal (Box-Muller) for the SecureBoost-shaped inputs */
+static double urand(unsigned long* s) {
+  *s ^= *s >> 12; *s ^= *s << 25; *s ^= *s >> 27;
+  return (double)((*s * 2685821657736338717ull) >> 11) * (1.0 / 9007199254740992.0);
+}
+static double nrand(unsigned long* s) {
+  const double u = urand(s) + 1e-300, v = urand(s);
+  return sqrt(-2.0 * log(u)) * cos(6.283185307179586 * v);
+}
+/* Coder::encode_f64 (fixedpoint_paillier/src/lib.rs:148-168) of a float32 value: base-16
+   exponent floor((frexp_e - 53) / 4) and the signed 53-bit significand x * 16^-exp (exact) */
+static int encode_exp(double x) {
+  int e;
+  if (x == 0.0) return -14;
+  (void)frexp(x, &e);
+  const int d = e - 53;
+  return d >= 0 ? d / 4 : -((-d + 3) / 4);
+}
+
+/* Ciphertext::add of `t` (exp te) into the slot (acc, ae): the literal-1 rule, the exponent
+   alignment of the higher operand by mpz_powm(x, 16^gap, n^2), then add_ct */
+static void fp_add_into(gref_ctx* c, mpz_struct* acc, int* ae, const mpz_struct* tc, int te, mpz_struct* t,
+                        mpz_struct* e16) {
+  if (acc->_mp_size == 1 && acc->_mp_d[0] == 1) {  /* literal 1: the slot becomes the term */
+    __gmpz_set(acc, tc);
+    *ae = te;
+    return;
+  }
+  if (*ae > te) {
+    __gmpz_set_ui(e16, 1);
+    __gmpz_mul_2exp(e16, e16, 4u * (unsigned)(*ae - te));
+    __gmpz_powm(acc, acc, e16, c->ns);
+    __gmpz_mul(t, acc, tc);
+    *ae = te;
+  } else if (*ae < te) {
+    __gmpz_set_ui(e16, 1);
+    __gmpz_mul_2exp(e16, e16, 4u * (unsigned)(te - *ae));
+    __gmpz_powm(t, tc, e16, c->ns);
+    __gmpz_mul(t, acc, t);
+  } else {
+    __gmpz_mul(t, acc, tc);
+  }
+  __gmpz_tdiv_r(acc, t, c->ns);
+}
 
 static double now_s(void) {
   struct timespec ts;
@@ -215,6 +267,20 @@ static void* run_job(void* arg) {
   /* a realistic ciphertext / operands */
   __gmpz_urandomm(acc, rs, c->ns);
   __gmpz_urandomm(o, rs, c->ns);
+  /* iupdate: 4 features x 32 bins x (g, h) slots (the bench's histogram shape), literal 1s at
+     first, and a pool of 64 source ciphertexts standing for the encrypted g and h */
+  enum { kSlots = 256, kPool = 64 };
+  mpz_struct* slot = NULL;
+  int* sexp = NULL;
+  mpz_struct* pool = NULL;
+  unsigned long xs = j->seed * 0x9E3779B97F4A7C15ull + 1;
+  if (j->op == 5) {
+    slot = (mpz_struct*)calloc(kSlots, sizeof(mpz_struct));
+    sexp = (int*)calloc(kSlots, sizeof(int));
+    pool = (mpz_struct*)calloc(kPool, sizeof(mpz_struct));
+    for (int k = 0; k < kSlots; ++k) { __gmpz_init(&slot[k]); __gmpz_set_ui(&slot[k], 1); }
+    for (int k = 0; k < kPool; ++k) { __gmpz_init(&pool[k]); __gmpz_urandomm(&pool[k], rs, c->ns); }
+  }
   double t0 = now_s();
   for (long i = 0; i < j->count; ++i) {
     if (j->op == 0) {
@@ -240,6 +306,30 @@ static void* run_job(void* arg) {
     } else if (j->op == 2) {
       __gmpz_mul(t, acc, o);
       __gmpz_tdiv_r(acc, t, c->ns);
+    } else if (j->op == 4) {
+      /* Ciphertext::mul by an encoded float32 weight w in [-1, 2) (encode_f32 widens to f64:
+         a <= 56-bit significand whose low 29 bits are zero); w < 0 (a third): GMP powm with a
+         negative exponent inverts the base first (math/src/rug/mod.rs:30-35) */
+      const double wv = urand(&xs) * 3.0 - 1.0;
+      const float wf = (float)wv;
+      const int ex = encode_exp((double)wf);
+      const double mag = ldexp(fabs((double)wf), -4 * ex);
+      __gmpz_set_ui(m, (unsigned long)mag);
+      if (wf < 0) {
+        __gmpz_invert(r, acc, c->ns);
+        __gmpz_powm(nude, r, m, c->ns);
+      } else {
+        __gmpz_powm(nude, acc, m, c->ns);
+      }
+    } else if (j->op == 5) {
+      /* iupdate: one scatter-add of a SecureBoost-shaped term (g = p - y or h = p (1 - p),
+         p = sigmoid(N(0, 1)), encoded float32 exponents) into a random slot */
+      const double pv = 1.0 / (1.0 + exp(-nrand(&xs)));
+      const int hterm = (int)(i & 1);
+      const double v = hterm ? pv * (1.0 - pv) : pv - (urand(&xs) < 0.5 ? 1.0 : 0.0);
+      const int te = encode_exp((double)(float)v);
+      const int k = (int)(urand(&xs) * (kSlots / 2)) * 2 + hterm;
+      fp_add_into(c, &slot[k], &sexp[k], &pool[i % kPool], te, t, m);
     } else {
       /* Ciphertext::add with exponent alignment (fixedpoint_paillier/src/lib.rs:301-333):
          decrese_exp_to (:250-258) raises the higher-exp operand to 16^gap through mul_pt
@@ -259,6 +349,11 @@ static void* run_job(void* arg) {
     }
   }
   j->secs = now_s() - t0;
+  if (j->op == 5) {
+    for (int k = 0; k < kSlots; ++k) __gmpz_clear(&slot[k]);
+    for (int k = 0; k < kPool; ++k) __gmpz_clear(&pool[k]);
+    free(slot); free(sexp); free(pool);
+  }
   __gmpz_clear(m); __gmpz_clear(nude); __gmpz_clear(r); __gmpz_clear(t); __gmpz_clear(acc);
   __gmpz_clear(dp); __gmpz_clear(dq); __gmpz_clear(o);
   __gmp_randclear(rs);

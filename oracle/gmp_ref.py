@@ -83,7 +83,7 @@ class GmpKey:
     def bench(self, op: str, per_thread: int, threads: int = 1, seed: int = 1) -> float:
         """Wall seconds for threads x per_thread elements of op in {'encrypt', 'decrypt', 'add',
         'add_gap'} ('add_gap': ct-add with the Hetero-LR exponent-gap mix, see gmp_ref.c)."""
-        code = {"encrypt": 0, "decrypt": 1, "add": 2, "add_gap": 3}[op]
+        code = {"encrypt": 0, "decrypt": 1, "add": 2, "add_gap": 3, "mul": 4, "iupdate": 5}[op]
         return load().gref_bench(self.ctx, code, per_thread, threads, seed)
 
 

@@ -5,7 +5,8 @@ bench.py rank does.  Prints one JSON line; exit status 0 iff every check passed.
 
 Checks (bit for bit):
   * gather_tiles / gather_ciphertexts of encrypted shards (whole tiles, a partial last tile,
-    an empty shard) return the shard itself, sign gathered as uint8;
+    an empty shard) return the shard itself, sign gathered as uint8, onto every rank and onto
+    one rank (gather_ciphertexts(dst=0));
   * compact_gathered on padded multi-rank buffers (whole-tile and ragged shard counts);
   * fold_across_ranks / fold_partials -- the cross-rank SecureBoost histogram fold -- against
     the sequential ct-add chain (k_add27) over the same partials and against the oracle.
@@ -55,6 +56,8 @@ def main() -> int:
             ok &= bool(torch.equal(eg[:n], cv.exp[:n]))
             gv = gather_ciphertexts(cv)
             ok &= gv.n == pk.n and gv.count == n
+            g0 = gather_ciphertexts(cv, dst=0)  # onto one rank: point-to-point (here: the rank itself)
+            ok &= g0.n == pk.n and g0.count == n and bool(torch.equal(g0.C[:nt], cv.C[:nt]))
             if n:
                 ok &= gv.to_signed_ints(pk.ns) == cv.to_signed_ints(pk.ns)
         res["gather"] = ok

@@ -8,7 +8,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from fate_amd.dist import WAVE, compact_gathered, gather_tiles, shard_bounds
+from fate_amd.dist import WAVE, compact_gathered, gather_tiles, gather_tiles_to, shard_bounds
 
 
 def test_shard_bounds_cover_and_align():
@@ -51,12 +51,19 @@ def _worker(rank, world, port, count, L, q):
             C[k // WAVE, :, k % WAVE] = torch.tensor([g * 1000 + j for j in range(L)], dtype=torch.int32)
             sign[k] = g % 2
             exp[k] = -(g % 7)
-        Cg, sg, eg, total = gather_tiles(C, sign, exp, n)
-        ok = total == count and sg.dtype == torch.uint8  # one byte of sign per element on the wire
-        for g in range(count):
-            ok &= bool(torch.equal(Cg[g // WAVE, :, g % WAVE],
-                                   torch.tensor([g * 1000 + j for j in range(L)], dtype=torch.int32)))
-            ok &= int(sg[g]) == g % 2 and int(eg[g]) == -(g % 7)
+        def check(Cg, sg, eg, total):
+            ok = total == count and sg.dtype == torch.uint8  # one byte of sign per element on the wire
+            for g in range(count):
+                ok &= bool(torch.equal(Cg[g // WAVE, :, g % WAVE],
+                                       torch.tensor([g * 1000 + j for j in range(L)], dtype=torch.int32)))
+                ok &= int(sg[g]) == g % 2 and int(eg[g]) == -(g % 7)
+            return ok
+
+        ok = check(*gather_tiles(C, sign, exp, n))
+        # the gather onto one rank (the federation sender): the full vector there, None elsewhere
+        for dst in range(world):
+            got = gather_tiles_to(C, sign, exp, n, dst)
+            ok &= (got is None) if rank != dst else check(*got)
         q.put((rank, ok))
     finally:
         dist.destroy_process_group()

@@ -1,7 +1,9 @@
 """Time the SecureBoost histogram leg of bench.py phase by phase (iupdate internals).
 With a third argument "mul", the terms are first multiplied by per-sample weights in
 [0.5, 1.5) (the weighted leg of tools/bench_legs/secureboost_full.py), which spreads their
-exponents."""
+exponents; with "edge", the first 8 gradients are bench.py's edge values (0, -0, +-1e-30,
++-3.4e38, +-1: exponent gaps up to 31 inside a slot, bench.py's histogram_edge_values).
+PHASES=0 times the whole call only (no synchronising wrappers: for kernel traces)."""
 import json
 import os
 import sys
@@ -29,13 +31,24 @@ if len(sys.argv) > 3 and sys.argv[3] == "mul":
     wts = (torch.rand(2 * N, generator=g) + 0.5).to(dev)
     gh = gh.mul(pk, coder.encode_f32_vec(wts))
     print(json.dumps({"distinct_exps": int(torch.unique(gh.exp[: 2 * N]).numel())}), flush=True)
+if len(sys.argv) > 3 and sys.argv[3] == "edge":
+    xe = torch.stack([(psig - ylab).float(), (psig * (1 - psig)).float()], 1).reshape(-1)
+    xe[:8] = torch.tensor([0.0, -0.0, 1e-30, -1e-30, 3.4e38, -3.4e38, 1.0, -1.0])
+    gh = pk.encrypt_encoded(coder.encode_f32_vec(xe.to(dev)), True)
+if len(sys.argv) > 3 and sys.argv[3] == "benchedge":
+    # bench.py's histogram_edge_values operands: its encrypt leg's x (randn * 4, seed 20241218,
+    # the edge values first) paired with 0.25 * flip(x)
+    xb = torch.randn(N, generator=torch.Generator().manual_seed(20241218), dtype=torch.float32) * 4
+    xb[:8] = torch.tensor([0.0, -0.0, 1e-30, -1e-30, 3.4e38, -3.4e38, 1.0, -1.0])
+    gh = pk.encrypt_encoded(coder.encode_f32_vec(torch.stack([xb, torch.flip(xb, [0]) * 0.25], 1).reshape(-1).to(dev)),
+                            True)
 bins = torch.randint(0, NB, (N, HF), generator=g)
 positions = bins + torch.arange(HF) * NB
 if os.environ.get("HIST_HOST_POSITIONS") != "1":
     positions = positions.to(dev, torch.int32)  # device-resident bin indexes (bench.py)
 T = {}
 orig = {name: getattr(P, name) for name in ("_fold_to_segments", "_fold_segments", "_fold_chunks", "_fold_tree", "_add",
-                                             "_add_order", "_flatten_positions", "_fit_limbs", "_fold_check")}
+                                             "_add_order", "_flatten_positions", "_fit_limbs", "_fold_failed")}
 
 
 def timed(name):
@@ -51,8 +64,9 @@ def timed(name):
     return w
 
 
-for name in orig:
-    setattr(P, name, timed(name))
+if os.environ.get("PHASES", "1") != "0":
+    for name in orig:
+        setattr(P, name, timed(name))
 for rep in range(2):
     T.clear()
     hist = P.CiphertextVector.zeros(HF * NB * 2, pk._key.L2, dev)

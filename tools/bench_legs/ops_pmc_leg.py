@@ -1,6 +1,9 @@
-"""One decrypt (2^18 elements) and one Hetero-LR-shaped ct-add (2^20 elements), 2048-bit key,
-for SQ / GRBM counter passes over k_pow_half27 and k_add27 (tools/gpu_job_ops_pmc.sh).
-Operands come from key-holder encryptions (the fast CRT path) so the setup stays short."""
+"""The op kernels once each, 2048-bit key, for rocprofv3 counter passes (tools/gpu_job.sh pmc):
+a decrypt of 2^18 elements, a Hetero-LR-shaped ct-add of 2^20, a ct x pt of 2^18 by float32
+weights in [-1, 2) (a third negative: the batch inverse runs), and the bench's histogram
+iupdate (1M samples x 4 features x (g, h) = 8.4M terms into 256 slots).  Operands come from
+key-holder encryptions (the fast CRT path) so the setup stays short.  Each kernel of these ops
+is dispatched once in this order (tools/pmc_ops_summary.py relies on it)."""
 import json
 import os
 import sys
@@ -20,12 +23,25 @@ g = torch.Generator().manual_seed(20241218)
 x = (torch.randn(N, generator=g) * 4).to(dev)
 a = pk.encrypt_encoded(coder.encode_f32_vec(x), True)
 b = pk.encrypt_encoded(coder.encode_f32_vec(torch.flip(x, [0]) * 0.25), True)
-torch.cuda.synchronize()
-t0 = time.perf_counter()
-d = sk.decrypt_to_encoded(a.slice(0, 1 << 18))
-torch.cuda.synchronize()
-t1 = time.perf_counter()
-s = a.add(pk, b)
-torch.cuda.synchronize()
-t2 = time.perf_counter()
-print(json.dumps({"decrypt_2^18_s": round(t1 - t0, 4), "add_2^20_s": round(t2 - t1, 4)}))
+w = coder.encode_f32_vec((torch.rand(1 << 18, generator=g) * 3.0 - 1.0).to(dev))
+HF, NB = 4, 32
+positions = (torch.randint(0, NB, (N, HF), generator=g) + torch.arange(HF) * NB).to(dev, torch.int32)
+t = {}
+
+
+def timed(name, f):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    r = f()
+    torch.cuda.synchronize()
+    t[name] = round(time.perf_counter() - t0, 4)
+    return r
+
+
+timed("decrypt_2^18_s", lambda: sk.decrypt_to_encoded(a.slice(0, 1 << 18)))
+timed("add_2^20_s", lambda: a.add(pk, b))
+timed("mul_2^18_s", lambda: a.slice(0, 1 << 18).mul(pk, w))
+gh = P.Evaluator.cat([a, b])._gather(torch.stack([torch.arange(N), N + torch.arange(N)], 1).reshape(-1))
+hist = P.CiphertextVector.zeros(HF * NB * 2, pk._key.L2, dev)
+timed("iupdate_8.4M_terms_s", lambda: hist.iupdate(gh, positions, 2, pk))
+print(json.dumps(t))

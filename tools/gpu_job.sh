@@ -1,10 +1,17 @@
-# Parameterised GPU job (replaces the round-1..3 one-off gpu_job_*.sh scripts).
-#   tools/gpu_job.sh TAG MODE [pytest-args...]
-# MODE: tests   the GPU test suite (no -x: every failure listed), args select tests
-#       round   tests + smoke + the default bench line
-#       bench   the default bench line only
-#       prof    rocprofv3 kernel trace + stats of a short bench run
-# Every GPU step runs under its own time limit; the script stops at the first abort.
+# Parameterised GPU job (replaces rounds 1-3's fifty one-off tools/gpu_job_*.sh scripts;
+# same-box A/B of library variants stays in tools/gpu_job_ab.sh).
+#   bash tools/gpu_job.sh TAG MODE [args...]
+# MODE  tests     the GPU test suite (no -x: every failure listed); args select tests
+#       round     tests + smoke + the default bench line (args go to bench.py)
+#       bench     the default bench line only (args go to bench.py)
+#       prof      rocprofv3 --kernel-trace --stats of a short bench run
+#       pmc       FETCH_SIZE / WRITE_SIZE passes (one counter per run): the encrypt kernel over
+#                 bench.py --n 131072, the op kernels over tools/bench_legs/ops_pmc_leg.py,
+#                 summarised into gpurun_out/TAG_pmc_encrypt27.json / TAG_pmc_ops.json
+#       sq        SQ / GRBM counter passes over tools/bench_legs/ops_pmc_leg.py
+#       evidence  round, then prof, then pmc (the end-of-round record for profiles/)
+#       leg       python tools/bench_legs/ARGS (one bench leg script)
+# Every GPU step runs under its own time limit and the script stops at the first failure.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 T=${1:?tag}
@@ -12,31 +19,61 @@ M=${2:-round}
 shift 2 || true
 cd $R
 mkdir -p gpurun_out
+
 run_tests() {
-  timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread "$@" > gpurun_out/${T}_tests.txt 2>&1
+  timeout -k 10 1200 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread "$@" > gpurun_out/${T}_tests.txt 2>&1
   local rc=$?
   grep -E "passed|failed|error" gpurun_out/${T}_tests.txt | tail -3
   grep -E "^FAILED|^ERROR" gpurun_out/${T}_tests.txt | head -40
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "tests aborted rc=$rc"; exit 1; fi
   echo tests_rc=$rc
 }
-run_bench() {
-  timeout -k 10 900 python -u bench.py "$@" > gpurun_out/${T}_bench.txt 2>&1 || { echo bench_failed; tail -30 gpurun_out/${T}_bench.txt; exit 1; }
-  tail -1 gpurun_out/${T}_bench.txt > gpurun_out/${T}_bench.json
-  python -c "import json;d=json.load(open('gpurun_out/${T}_bench.json'));print(d['value'], d['roofline']['frac'], {k: d.get(k) for k in ('decrypt_per_s','ct_add_per_s','ct_mul_per_s','histogram_iupdate_s')})"
+run_smoke() {
+  timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${T}_smoke.log 2>&1 || { echo smoke_failed; tail -20 gpurun_out/${T}_smoke.log; exit 1; }
+  tail -1 gpurun_out/${T}_smoke.log
 }
+run_bench() {
+  timeout -k 10 1000 python -u bench.py "$@" > gpurun_out/${T}_bench.txt 2>&1 || { echo bench_failed; tail -30 gpurun_out/${T}_bench.txt; exit 1; }
+  tail -1 gpurun_out/${T}_bench.txt > gpurun_out/${T}_bench.json
+  python tools/bench_summary.py gpurun_out/${T}_bench.json
+}
+run_prof() {
+  (cd /tmp && export TMPDIR=/tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/${T}_trace -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline "$@" > $R/gpurun_out/${T}_trace_bench.txt 2>&1) || { echo trace_failed; tail -20 gpurun_out/${T}_trace_bench.txt; exit 1; }
+  tail -1 gpurun_out/${T}_trace_bench.txt > gpurun_out/${T}_trace_bench.json
+  echo prof_ok
+}
+pmc_pass() {  # pmc_pass NAME COUNTER CMD...
+  local name=$1 counter=$2
+  shift 2
+  (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 300 rocprofv3 --pmc $counter --output-format csv -d $R/gpurun_out/${T}_${name} -o run -- "$@" > $R/gpurun_out/${T}_${name}.txt 2>&1) || { echo pmc_${name}_failed; tail -20 gpurun_out/${T}_${name}.txt; exit 1; }
+}
+run_pmc() {
+  pmc_pass pmc_fetch FETCH_SIZE python3 $R/bench.py --n 131072 --steps 1 --warmup 0 --no-extras --no-cpu-baseline
+  pmc_pass pmc_write WRITE_SIZE python3 $R/bench.py --n 131072 --steps 1 --warmup 0 --no-extras --no-cpu-baseline
+  python tools/pmc_summary.py gpurun_out/$T gpurun_out/${T}_pmc_encrypt27.json > /dev/null || exit 1
+  pmc_pass fetch FETCH_SIZE python3 $R/tools/bench_legs/ops_pmc_leg.py
+  pmc_pass write WRITE_SIZE python3 $R/tools/bench_legs/ops_pmc_leg.py
+  python tools/pmc_ops_summary.py gpurun_out/$T gpurun_out/${T}_pmc_ops.json || exit 1
+  grep hbm_bytes_per_elem gpurun_out/${T}_pmc_encrypt27.json
+}
+run_sq() {
+  pmc_pass sq "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE GRBM_COUNT" python3 $R/tools/bench_legs/ops_pmc_leg.py
+  pmc_pass sq2 "SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_LDS_BANK_CONFLICT SQ_INSTS_BRANCH" python3 $R/tools/bench_legs/ops_pmc_leg.py
+  echo sq_ok
+}
+
 case $M in
   tests) run_tests "$@" ;;
-  round)
-    run_tests "$@"
-    timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${T}_smoke.log 2>&1 || { echo smoke_failed; tail -20 gpurun_out/${T}_smoke.log; exit 1; }
-    tail -1 gpurun_out/${T}_smoke.log
-    run_bench ;;
+  round) run_tests; run_smoke; run_bench "$@" ;;
   bench) run_bench "$@" ;;
-  prof)
-    cd /tmp && export TMPDIR=/tmp && cd $R
-    timeout -k 10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_prof -o run -- python3 -u bench.py "$@" > gpurun_out/${T}_prof_bench.txt 2>&1 || { echo prof_failed; tail -30 gpurun_out/${T}_prof_bench.txt; exit 1; }
-    tail -1 gpurun_out/${T}_prof_bench.txt > gpurun_out/${T}_prof_bench.json
-    find gpurun_out/${T}_prof -name "*kernel_stats.csv" | head -3 ;;
+  prof) run_prof "$@" ;;
+  pmc) run_pmc ;;
+  sq) run_sq ;;
+  evidence) run_tests; run_smoke; run_bench "$@"; run_prof; run_pmc ;;
+  leg)
+    L=$1; shift
+    timeout -k 10 900 python -u tools/bench_legs/$L "$@" > gpurun_out/${T}_leg.txt 2>&1 || { echo leg_failed; tail -30 gpurun_out/${T}_leg.txt; exit 1; }
+    tail -5 gpurun_out/${T}_leg.txt ;;
   *) echo "unknown mode $M"; exit 2 ;;
 esac
+echo all_ok

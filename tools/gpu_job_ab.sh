@@ -1,19 +1,24 @@
-# same-box A/B of the encrypt leg: tools/gpu_job_ab.sh TAG VARIANT... (fate_amd/lib/ab/lib_<V>.so;
-# "main" = fate_amd/lib/libfatephe.so).  Each variant: parity tests, then two alternating bench runs.
+# Same-box A/B of library variants: tools/gpu_job_ab.sh TAG [--no-tests] VARIANT...
+# (fate_amd/lib/ab/lib_<V>.so; "main" = fate_amd/lib/libfatephe.so).  Each variant: the parity
+# tests (unless --no-tests: a variant from before an ABI change), then two alternating
+# encrypt-only bench runs.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R
 mkdir -p gpurun_out
 T=$1; shift
-for V in "$@"; do
-  L=$R/fate_amd/lib/ab/lib_$V.so; [ "$V" = main ] && L=$R/fate_amd/lib/libfatephe.so
-  FPHE_LIB_PATH=$L timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/${T}_${V}_tests.txt 2>&1 || { echo tests_failed $V; tail -30 gpurun_out/${T}_${V}_tests.txt; exit 1; }
-done
+TESTS=1
+if [ "$1" = "--no-tests" ]; then TESTS=0; shift; fi
+lib_of() { if [ "$1" = main ]; then echo $R/fate_amd/lib/libfatephe.so; else echo $R/fate_amd/lib/ab/lib_$1.so; fi; }
+if [ $TESTS = 1 ]; then
+  for V in "$@"; do
+    FPHE_LIB_PATH=$(lib_of $V) timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/${T}_${V}_tests.txt 2>&1 || { echo tests_failed $V; tail -30 gpurun_out/${T}_${V}_tests.txt; exit 1; }
+  done
+fi
 for rep in 1 2; do
   for V in "$@"; do
-    L=$R/fate_amd/lib/ab/lib_$V.so; [ "$V" = main ] && L=$R/fate_amd/lib/libfatephe.so
-    FPHE_LIB_PATH=$L timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-extras > gpurun_out/${T}_${V}_b$rep.txt 2>&1 || { echo bench_failed $V; tail -30 gpurun_out/${T}_${V}_b$rep.txt; exit 1; }
-    python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['value'], d['roofline']['issue']['frac'])" gpurun_out/${T}_${V}_b$rep.txt $V
+    FPHE_LIB_PATH=$(lib_of $V) timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-extras > gpurun_out/${T}_${V}_b$rep.txt 2>&1 || { echo bench_failed $V; tail -30 gpurun_out/${T}_${V}_b$rep.txt; exit 1; }
+    python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['value'], d['roofline']['frac'], d['roofline']['kernel_ms'])" gpurun_out/${T}_${V}_b$rep.txt $V
   done
 done
 echo all_ok

@@ -1,10 +1,11 @@
-"""HBM traffic of the decrypt and ct-add kernels from FETCH_SIZE / WRITE_SIZE passes over
-tools/bench_legs/ops_pmc_leg.py (tools/gpu_job_ops_traffic.sh): decrypt of 2^18 elements
+"""HBM traffic of the decrypt, ct-add, ct x pt and iupdate kernels from FETCH_SIZE / WRITE_SIZE
+passes over tools/bench_legs/ops_pmc_leg.py (tools/gpu_job.sh pmc): decrypt of 2^18 elements
 (k_pow_half27<128, 6, false> + k_decrypt_crt<128>), the Hetero-LR-shaped ct-add of 2^20
-(k_add27<128>), 2048-bit key.  FETCH_SIZE doubled per the calibration probe
+(k_add27<128>), ct x pt of 2^18 (classify, batch inverse, k_mul27), the histogram fold's copy
+and balanced level over 8.4M terms, 2048-bit key.  FETCH_SIZE doubled per the calibration probe
 (tools/probe/fetch_calib.hip: one dword per lane over 256-B rows, the pattern of these
 kernels' ColIO / whole-vector descriptor accesses).  bench.py reports the result as the
-`traffic` of rooflines.decrypt / rooflines.ct_add.
+`traffic` of rooflines.decrypt / ct_add / ct_mul / iupdate.
 
     python tools/pmc_ops_summary.py gpurun_out/TAG profiles/r02/TAG_pmc_ops.json
 """
@@ -15,7 +16,13 @@ import sys
 
 KERNELS = {"decrypt": (["k_pow_half27<128, 6, false>", "k_decrypt_crt<128>"], 1 << 18,
                        "algorithmic: read 512 B C (+ sign/exp), write 4-256 B plaintext"),
-           "ct_add": (["k_add27<128>"], 1 << 20, "algorithmic: two 517-B operands read, one written (+4-B order)")}
+           "ct_add": (["k_add27<128>"], 1 << 20, "algorithmic: two 517-B operands read, one written (+4-B order)"),
+           "ct_mul": (["k_mul_prep<128>", "k_binv_pre27<128>", "k_inv_n27<128>", "k_inv_lift27<128>",
+                       "k_binv_post27<128>", "k_mul27<128, 4>"], 1 << 18,
+                      "algorithmic: one 517-B operand and a 13-B plaintext read, 517 B written"),
+           "iupdate": (["k_tiles_to_rows<128>", "k_segfold27<128, true>"], 8 << 20,
+                       "per term: the source row copy (element-major, once per source element) and the "
+                       "balanced fold level, which gathers one 512-B row per term (algorithmic: 517 B per term)")}
 
 
 def per_kernel(path, counter):
@@ -35,10 +42,12 @@ def main(prefix, out):
         rd = wr = 0.0
         detail = {}
         for k in kerns:
-            fk = [v for (kn, _), v in f.items() if k in kn]
-            wk = [v for (kn, _), v in w.items() if k in kn]
+            # the first dispatch of the kernel in the leg's order (the iupdate's final add is a
+            # second k_add27 dispatch, after the ct-add leg's)
+            fk = [v for (kn, d), v in sorted(f.items(), key=lambda kv: int(kv[0][1])) if k in kn][:1]
+            wk = [v for (kn, d), v in sorted(w.items(), key=lambda kv: int(kv[0][1])) if k in kn][:1]
             if len(fk) != 1 or len(wk) != 1:
-                raise SystemExit(f"expected one {k} dispatch per pass, found {len(fk)}/{len(wk)}")
+                raise SystemExit(f"expected a {k} dispatch in each pass, found {len(fk)}/{len(wk)}")
             detail[k] = {"FETCH_SIZE_KiB": fk[0], "WRITE_SIZE_KiB": wk[0]}
             rd += fk[0] * 1024 * 2.0
             wr += wk[0] * 1024

@@ -1,4 +1,4 @@
-"""Per-kernel SQ counter table from rocprofv3 --pmc csv passes (tools/gpu_job_segpmc.sh):
+"""Per-kernel SQ counter table from rocprofv3 --pmc csv passes (tools/gpu_job.sh sq):
     python tools/pmc_sq_compare.py gpurun_out/TAG_h1 gpurun_out/TAG_h2 ... [--match k_segfold27 k_probe]
 prints, per kernel name fragment, the counters summed over its dispatches and the derived
 rates (VALU instructions per wave-cycle, wait fractions)."""

@@ -1,4 +1,4 @@
-"""Turn the FETCH_SIZE / WRITE_SIZE rocprofv3 passes (tools/gpu_job_prof.sh) into the per-element
+"""Turn the FETCH_SIZE / WRITE_SIZE rocprofv3 passes (tools/gpu_job.sh pmc) into the per-element
 HBM traffic json that bench.py reports as roofline.traffic.
 
     python tools/pmc_summary.py gpurun_out/r01d profiles/r01d_pmc_encrypt27.json [elements]
