@@ -310,12 +310,15 @@ def _resolve(v: "CiphertextVector", n: int) -> None:
 
 
 def _resolve_args(n: int, *objs) -> None:
+    """Give every key-less vector among an operation's arguments its key.  Sequences are entered
+    only when they hold vectors (cat's list, iadd_slice's ciphertexts): a histogram's position
+    lists (Vec<Vec<usize>>) are never walked element by element."""
     for a in objs:
         if isinstance(a, CiphertextVector):
             _resolve(a, n)
         elif isinstance(a, Ciphertext):
             _resolve(a.vec, n)
-        elif isinstance(a, (list, tuple)):
+        elif isinstance(a, (list, tuple)) and a and isinstance(a[0], (CiphertextVector, Ciphertext)):
             _resolve_args(n, *a)
 
 
@@ -816,11 +819,18 @@ class CiphertextVector:
         if ii.numel() == 0:
             return
         dev = self.device
-        # int32 index arithmetic when every source row and slot fits (fphe_fold_segments takes
-        # int32 indexes): half the bytes of the int64 expansion on 8M-term histograms
-        it = torch.int32 if max(other.count, self.count) * max(stride, 1) < (1 << 31) else torch.int64
-        ii, pp = ii.to(dev, it), pp.to(dev, it)
-        t = torch.arange(stride, device=dev, dtype=it)
+        stride = max(int(stride), 1)
+        # positions are usize in the reference: out of [0, len / stride) it panics on the index
+        # (lib.rs:724-735).  Checked in 64 bits before any narrowing, so a huge position cannot
+        # wrap onto a valid slot; the samples likewise against `other`
+        lo, hi = torch.aminmax(pp.to(torch.int64))
+        lo, hi, imax = torch.stack([lo, hi, ii.max().to(torch.int64)]).tolist()  # one read-back
+        if lo < 0 or (hi + 1) * stride > self.count or (imax + 1) * stride > other.count:
+            raise PanicException("index out of bounds")
+        # int32 index arithmetic (fphe_fold_segments takes int32 indexes): half the bytes of the
+        # int64 expansion on 8M-term histograms; every value is now < 2^31
+        ii, pp = ii.to(dev, torch.int32), pp.to(dev, torch.int32)
+        t = torch.arange(stride, device=dev, dtype=torch.int32)
         src = (ii[:, None] * stride + t).reshape(-1)
         slot = (pp[:, None] * stride + t).reshape(-1)
         # one ciphertext per slot (the literal 1 where no term lands: add's identity), then
@@ -1074,23 +1084,25 @@ def _add(pk: "PK", a: CiphertextVector, b: CiphertextVector, broadcast: bool, co
 
 
 def _flatten_positions(indexes, dev=None) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Vec<Vec<usize>> of positions per sample -> (sample ids, positions), flat int32 on `dev`.
-    A [samples, positions] tensor is expanded on the device (no host-side index arrays)."""
+    """Vec<Vec<usize>> of positions per sample -> (sample ids, positions), flat on `dev`: sample
+    ids int64, positions in their own integer type (int32 for a device int32 tensor), range-checked
+    and narrowed by the caller (:meth:`CiphertextVector._scatter_fold`).  A [samples, positions]
+    tensor is expanded on the device (no host-side index arrays)."""
     if isinstance(indexes, torch.Tensor):
         if indexes.dim() != 2:
             raise ValueError("positions tensor must be 2-D [samples, positions]")
         ns, npos = indexes.shape
-        if (ns * npos) >= (1 << 31):
-            raise ValueError("iupdate: more than 2^31 - 1 positions in one call")
-        pp = indexes.to(device=dev, dtype=torch.int32).reshape(-1)
-        ii = torch.arange(ns * npos, device=dev, dtype=torch.int32) // max(npos, 1)
+        pp = indexes.to(device=dev).reshape(-1)
+        if pp.dtype not in (torch.int32, torch.int64):
+            pp = pp.to(torch.int64)
+        ii = torch.arange(ns * npos, device=dev, dtype=torch.int64) // max(npos, 1)
         return ii, pp
     lens = [len(x) for x in indexes]
     if sum(lens) == 0:
-        return torch.zeros(0, dtype=torch.int32, device=dev), torch.zeros(0, dtype=torch.int32, device=dev)
+        return torch.zeros(0, dtype=torch.int64, device=dev), torch.zeros(0, dtype=torch.int64, device=dev)
     ii = torch.arange(len(lens)).repeat_interleave(torch.tensor(lens))
     pp = torch.tensor(list(itertools.chain.from_iterable(indexes)), dtype=torch.long)
-    return ii.to(dev, torch.int32), pp.to(dev, torch.int32)
+    return ii.to(dev), pp.to(dev)
 
 
 ADD_REGIONS = 8  # kAddRegions in fate_phe.hip: runs of k_add27 wave tiles, one per XCD
@@ -1211,10 +1223,12 @@ def _fold_to_segments(pk: "PK", src: CiphertextVector, seg: torch.Tensor, nseg: 
     (the caller then calls :func:`_fold_failed` once its follow-up launches are queued, and
     folds with :func:`_fold_dense` if it reports a gap beyond the device merge's range)."""
     dev = src.device
+    T = seg.numel()
+    if T > FOLD_MAX_TERMS:
+        return _fold_chunked(pk, src, seg, nseg, index, with_present)
     src = _fit_limbs(src, pk._key.L2)
     L2 = pk._key.L2
     seg = seg.to(dev, torch.int32).contiguous()
-    T = seg.numel()
     idx = None if index is None else index.to(dev, torch.int32).contiguous()
     if idx is not None and idx.numel() != T:
         raise ValueError("fold: index and segment arrays differ in length")
@@ -1239,6 +1253,36 @@ def _fold_to_segments(pk: "PK", src: CiphertextVector, seg: torch.Tensor, nseg: 
         deferred.append(err)
     elif _fold_failed([err]):
         out, present = _fold_dense(pk, src, seg, nseg, idx)
+    return (out, present) if with_present else out
+
+
+# fphe_fold_segments counts its terms in int32 (include/fate_phe.h): a longer term list is
+# folded in chunks of this many (module-level so the GPU tests can exercise the split small)
+FOLD_MAX_TERMS = (1 << 31) - 1
+
+
+def _fold_chunked(pk: "PK", src: CiphertextVector, seg: torch.Tensor, nseg: int,
+                  index: Optional[torch.Tensor], with_present: bool):
+    """_fold_to_segments over more than FOLD_MAX_TERMS terms: fold consecutive chunks and add
+    each chunk's per-segment result onto the running one where both hold terms.  The reference's
+    fold is sequential, so fold(t_1..t_k) = add(fold(t_1..t_j), fold(t_j+1..t_k)) with add's
+    literal-1 rule giving the right exponent when either side folded to the literal 1; a segment
+    a chunk does not reach keeps its running value."""
+    out = present = None
+    for a in range(0, seg.numel(), FOLD_MAX_TERMS):
+        b = min(a + FOLD_MAX_TERMS, seg.numel())
+        f, p = _fold_to_segments(pk, src, seg[a:b], nseg, None if index is None else index[a:b], with_present=True)
+        if out is None:
+            out, present = f, p
+            continue
+        r = _add(pk, out, f, broadcast=False)
+        both = (present != 0) & (p != 0)
+        take = torch.where(both, 2, torch.where(p != 0, 1, 0))[: r.sign.numel()]
+        pick = lambda x0, x1, x2, t: torch.where(t == 2, x2, torch.where(t == 1, x1, x0))
+        out.C = pick(out.C, f.C, r.C, take.view(-1, 1, WAVE))
+        out.sign = pick(out.sign, f.sign, r.sign, take)
+        out.exp = pick(out.exp, f.exp, r.exp, take)
+        present = present | p
     return (out, present) if with_present else out
 
 

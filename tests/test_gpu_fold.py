@@ -152,3 +152,42 @@ def test_iupdate_tensor_positions_device(env):
     od2 = list(data)
     O.iupdate_with_masks(opk, od2, src, pos[:k].tolist(), masks, 2)
     assert host(pk, hist2) == [(c.c, c.exp) for c in od2]
+
+
+def test_fold_chunked_past_term_limit(env, monkeypatch):
+    """More terms than fphe_fold_segments' int32 count: the fold runs in chunks added onto the
+    running result (literal-1 segments, segments a chunk misses, and segments only a later chunk
+    reaches included).  The limit is lowered to 97 terms so the split is exercised at test size."""
+    fx, sk, pk, coder, opk, cts = env
+    rng = random.Random(17)
+    src = mixed_sources(opk, cts, 150, 17)
+    nseg = 19
+    T = 500
+    idx = [rng.randrange(len(src)) for _ in range(T)]
+    seg = [rng.randrange(nseg - 4) for _ in range(T)]
+    lits = [i for i, c in enumerate(src) if c.c == 1]
+    idx += lits[:3]
+    seg += [nseg - 3] * len(lits[:3])  # only the last chunk reaches this all-literal segment
+    want = oracle_fold(opk, src, idx, seg, nseg)
+    monkeypatch.setattr(P, "FOLD_MAX_TERMS", 97)
+    got, present = P._fold_to_segments(pk, dev_vec(pk, src), torch.tensor(seg), nseg, index=torch.tensor(idx),
+                                       with_present=True)
+    assert host(pk, got) == want
+    assert present[:nseg].tolist() == [int(s in set(seg)) for s in range(nseg)]
+    hist = dev_vec(pk, mixed_sources(opk, cts, 2 * nseg, 171))
+    od = [O.Ciphertext(c[0], c[1]) for c in host(pk, hist)]
+    pos = [[rng.randrange(nseg) for _ in range(4)] for _ in range(60)]
+    hist.iupdate(dev_vec(pk, src[:120]), pos, 2, pk)
+    O.iupdate(opk, od, src[:120], pos, 2)
+    assert host(pk, hist) == [(c.c, c.exp) for c in od]
+
+
+def test_iupdate_position_range_checked_before_narrowing(env):
+    """Positions are usize in the reference: one past the histogram panics, and so does one that
+    would wrap onto a valid slot if narrowed to int32 first (2^32 + 1 -> 1)."""
+    fx, sk, pk, coder, opk, cts = env
+    v = dev_vec(pk, more(opk, cts, 4))
+    hist = P.CiphertextVector.zeros(4, pk._key.L2)
+    for bad in ([[0], [(1 << 32) + 1]], torch.tensor([[0], [(1 << 32) + 1]]), torch.tensor([[0], [-1]])):
+        with pytest.raises(P.PanicException):
+            hist.iupdate(v, bad, 1, pk)
