@@ -7,9 +7,11 @@ same method names, argument meaning and error behaviour, over :mod:`fate_amd.pai
 ``PHECipherBuilder.setup`` imports ``fate.arch.protocol.phe.paillier``
 (python/fate/arch/context/_cipher.py:111-124); see INTEGRATION.md.
 
-Differences by design: tensors may be CUDA (HIP) tensors -- encoding reads them in place
-in HBM instead of calling ``.numpy()`` (paillier.py:159-161), and decoding returns a
-tensor on the requested device.
+Route A (:mod:`fate_amd.compat`) runs FATE's own adapter file unchanged; this module is
+Route B and keeps only what differs from that file: tensors may be CUDA (HIP) tensors --
+encoding reads them in place in HBM instead of calling ``.numpy()`` (paillier.py:159-161),
+decoding returns a tensor on the requested device -- and :func:`supports` gates key sizes.
+The pass-through methods are generated from name tables rather than written out.
 """
 from __future__ import annotations
 
@@ -44,6 +46,16 @@ class PK:
         return self.pk.encrypt_encoded_scalar(val, obfuscate)
 
 
+# dtype -> the fate_utils Coder method suffix (paillier.py:79-93, 128-140)
+_SUFFIX = {torch.float64: "f64", torch.float32: "f32", torch.int64: "i64", torch.int32: "i32"}
+
+
+def _suffix(dtype) -> str:
+    if dtype not in _SUFFIX:
+        raise NotImplementedError(f"{dtype} not supported")
+    return _SUFFIX[dtype]
+
+
 class Coder:
     def __init__(self, coder: _p.Coder):
         self.coder = coder
@@ -73,89 +85,37 @@ class Coder:
             dtype = vec.dtype
         elif dtype != vec.dtype:
             vec = vec.to(dtype=dtype)
-        if dtype == torch.float64:
-            return self.coder.encode_f64_vec(vec)
-        if dtype == torch.float32:
-            return self.coder.encode_f32_vec(vec)
-        if dtype == torch.int64:
-            return self.coder.encode_i64_vec(vec)
-        if dtype == torch.int32:
-            return self.coder.encode_i32_vec(vec)
-        raise NotImplementedError(f"{vec.dtype} not supported")
+        return getattr(self, f"encode_{_suffix(dtype)}_vec")(vec)
 
     def decode_vec(self, vec: FV, dtype: torch.dtype) -> V:
-        if dtype == torch.float64:
-            return self.coder.decode_f64_vec(vec).cpu()
-        if dtype == torch.float32:
-            return self.coder.decode_f32_vec(vec).cpu()
-        if dtype == torch.int64:
-            return torch.tensor(self.coder.decode_i64_vec(vec), dtype=torch.int64)
-        if dtype == torch.int32:
-            return torch.tensor(self.coder.decode_i32_vec(vec), dtype=torch.int32)
-        raise NotImplementedError(f"{dtype} not supported")
+        return getattr(self, f"decode_{_suffix(dtype)}_vec")(vec)
 
     def encode(self, val, dtype=None):
         if isinstance(val, torch.Tensor):
             assert val.ndim == 0, "only scalar supported"
             dtype = val.dtype
             val = val.item()
-        if dtype == torch.float64:
-            return self.coder.encode_f64(val)
-        if dtype == torch.float32:
-            return self.coder.encode_f32(val)
-        if dtype == torch.int64:
-            return self.coder.encode_i64(val)
-        if dtype == torch.int32:
-            return self.coder.encode_i32(val)
-        raise NotImplementedError(f"{dtype} not supported")
+        return getattr(self.coder, f"encode_{_suffix(dtype)}")(val)
 
-    def encode_f64(self, val: float):
-        return self.coder.encode_f64(val)
 
-    def decode_f64(self, val):
-        return self.coder.decode_f64(val)
+def _coder_methods() -> None:
+    """encode_X / decode_X pass through; encode_X_vec flattens the (device) tensor in place;
+    decode_X_vec returns a CPU tensor, as paillier.py's torch.tensor does (paillier.py:141-171:
+    integer lists become int64 tensors, decode_vec included)."""
+    for sfx in _SUFFIX.values():
+        for kind in ("encode", "decode"):
+            name = f"{kind}_{sfx}"
+            setattr(Coder, name, lambda self, val, _n=name: getattr(self.coder, _n)(val))
+        setattr(Coder, f"encode_{sfx}_vec",
+                lambda self, vec, _n=f"encode_{sfx}_vec": getattr(self.coder, _n)(vec.detach().flatten()))
+        if sfx in ("f64", "f32"):
+            dec = lambda self, vec, _n=f"decode_{sfx}_vec": getattr(self.coder, _n)(vec).cpu()
+        else:
+            dec = lambda self, vec, _n=f"decode_{sfx}_vec": torch.tensor(getattr(self.coder, _n)(vec))
+        setattr(Coder, f"decode_{sfx}_vec", dec)
 
-    def encode_i64(self, val: int):
-        return self.coder.encode_i64(val)
 
-    def decode_i64(self, val):
-        return self.coder.decode_i64(val)
-
-    def encode_f32(self, val: float):
-        return self.coder.encode_f32(val)
-
-    def decode_f32(self, val):
-        return self.coder.decode_f32(val)
-
-    def encode_i32(self, val: int):
-        return self.coder.encode_i32(val)
-
-    def decode_i32(self, val):
-        return self.coder.decode_i32(val)
-
-    def encode_f64_vec(self, vec: torch.Tensor):
-        return self.coder.encode_f64_vec(vec.detach().flatten())
-
-    def decode_f64_vec(self, vec):
-        return self.coder.decode_f64_vec(vec).cpu()
-
-    def encode_i64_vec(self, vec: torch.Tensor):
-        return self.coder.encode_i64_vec(vec.detach().flatten())
-
-    def decode_i64_vec(self, vec):
-        return torch.tensor(self.coder.decode_i64_vec(vec))
-
-    def encode_f32_vec(self, vec: torch.Tensor):
-        return self.coder.encode_f32_vec(vec.detach().flatten())
-
-    def decode_f32_vec(self, vec):
-        return self.coder.decode_f32_vec(vec).cpu()
-
-    def encode_i32_vec(self, vec: torch.Tensor):
-        return self.coder.encode_i32_vec(vec.detach().flatten())
-
-    def decode_i32_vec(self, vec):
-        return torch.tensor(self.coder.decode_i32_vec(vec))
+_coder_methods()
 
 
 def supports(key_size: int) -> bool:
@@ -171,84 +131,33 @@ def keygen(key_size):
     return SK(sk), PK(pk), Coder(coder)
 
 
+def _encrypted(b, pk: PK, coder: Coder, output_dtype, scalar: bool) -> EV:
+    """The plain operand of add/sub/rsub_plain(_scalar): encoded, encrypted without
+    obfuscation (paillier.py:187-262)."""
+    if scalar:
+        return pk.encrypt_encoded_scalar(coder.encode(b, dtype=output_dtype), obfuscate=False)
+    return pk.encrypt_encoded(coder.encode_tensor(b, dtype=output_dtype or b.dtype), obfuscate=False)
+
+
 class evaluator:
-    """paillier.py:179-399 (TensorEvaluator[EV, V, PK, Coder])."""
-
-    @staticmethod
-    def add(a: EV, b: EV, pk: PK):
-        return a.add(pk.pk, b)
-
-    @staticmethod
-    def add_plain(a: EV, b: V, pk: PK, coder: Coder, output_dtype=None):
-        if output_dtype is None:
-            output_dtype = b.dtype
-        encoded = coder.encode_tensor(b, dtype=output_dtype)
-        encrypted = pk.encrypt_encoded(encoded, obfuscate=False)
-        return a.add(pk.pk, encrypted)
-
-    @staticmethod
-    def add_plain_scalar(a: EV, b, pk: PK, coder: Coder, output_dtype):
-        encoded = coder.encode(b, dtype=output_dtype)
-        encrypted = pk.encrypt_encoded_scalar(encoded, obfuscate=False)
-        return a.add_scalar(pk.pk, encrypted)
-
-    @staticmethod
-    def sub(a: EV, b: EV, pk: PK):
-        return a.sub(pk.pk, b)
-
-    @staticmethod
-    def sub_plain(a: EV, b: V, pk: PK, coder: Coder, output_dtype=None):
-        if output_dtype is None:
-            output_dtype = b.dtype
-        encoded = coder.encode_tensor(b, dtype=output_dtype)
-        encrypted = pk.encrypt_encoded(encoded, obfuscate=False)
-        return a.sub(pk.pk, encrypted)
-
-    @staticmethod
-    def sub_plain_scalar(a: EV, b, pk: PK, coder: Coder, output_dtype):
-        encoded = coder.encode(b, dtype=output_dtype)
-        encrypted = pk.encrypt_encoded_scalar(encoded, obfuscate=False)
-        return a.sub_scalar(pk.pk, encrypted)
-
-    @staticmethod
-    def rsub(a: EV, b: EV, pk: PK):
-        return a.rsub(pk.pk, b)
-
-    @staticmethod
-    def rsub_plain(a: EV, b: V, pk: PK, coder: Coder, output_dtype=None):
-        if output_dtype is None:
-            output_dtype = b.dtype
-        encoded = coder.encode_tensor(b, dtype=output_dtype)
-        encrypted = pk.encrypt_encoded(encoded, obfuscate=False)
-        return a.rsub(pk.pk, encrypted)
-
-    @staticmethod
-    def rsub_plain_scalar(a: EV, b, pk: PK, coder: Coder, output_dtype):
-        encoded = coder.encode(b, dtype=output_dtype)
-        encrypted = pk.encrypt_encoded_scalar(encoded, obfuscate=False)
-        return a.rsub_scalar(pk.pk, encrypted)
+    """paillier.py:179-399 (TensorEvaluator[EV, V, PK, Coder]).  add / sub / rsub and their
+    _plain / _plain_scalar forms are generated below."""
 
     @staticmethod
     def mul_plain(a: EV, b: V, pk: PK, coder: Coder, output_dtype=None):
-        if output_dtype is None:
-            output_dtype = b.dtype
-        encoded = coder.encode_tensor(b, dtype=output_dtype)
-        return a.mul(pk.pk, encoded)
+        return a.mul(pk.pk, coder.encode_tensor(b, dtype=output_dtype or b.dtype))
 
     @staticmethod
     def mul_plain_scalar(a: EV, b, pk: PK, coder: Coder, output_dtype):
-        encoded = coder.encode(b, dtype=output_dtype)
-        return a.mul_scalar(pk.pk, encoded)
+        return a.mul_scalar(pk.pk, coder.encode(b, dtype=output_dtype))
 
     @staticmethod
     def matmul(a: EV, b: V, a_shape, b_shape, pk: PK, coder: Coder, output_dtype):
-        encoded = coder.encode_tensor(b, dtype=output_dtype)
-        return a.matmul(pk.pk, encoded, a_shape, b_shape)
+        return a.matmul(pk.pk, coder.encode_tensor(b, dtype=output_dtype), a_shape, b_shape)
 
     @staticmethod
     def rmatmul(a: EV, b: V, a_shape, b_shape, pk: PK, coder: Coder, output_dtype):
-        encoded = coder.encode_tensor(b, dtype=output_dtype)
-        return a.rmatmul(pk.pk, encoded, a_shape, b_shape)
+        return a.rmatmul(pk.pk, coder.encode_tensor(b, dtype=output_dtype), a_shape, b_shape)
 
     @staticmethod
     def zeros(size, dtype) -> EV:
@@ -307,3 +216,19 @@ class evaluator:
     @staticmethod
     def cat(list: List[EV]) -> EV:
         return _p.Evaluator.cat(list)
+
+
+def _evaluator_arith() -> None:
+    """add / sub / rsub (EV op EV), op_plain (tensor; output_dtype defaults to b.dtype) and
+    op_plain_scalar (scalar) -- paillier.py:183-262, one pattern per op."""
+    for op in ("add", "sub", "rsub"):
+        setattr(evaluator, op, staticmethod(lambda a, b, pk, _o=op: getattr(a, _o)(pk.pk, b)))
+        setattr(evaluator, f"{op}_plain", staticmethod(
+            lambda a, b, pk, coder, output_dtype=None, _o=op:
+            getattr(a, _o)(pk.pk, _encrypted(b, pk, coder, output_dtype, False))))
+        setattr(evaluator, f"{op}_plain_scalar", staticmethod(
+            lambda a, b, pk, coder, output_dtype, _o=op:
+            getattr(a, f"{_o}_scalar")(pk.pk, _encrypted(b, pk, coder, output_dtype, True))))
+
+
+_evaluator_arith()
