@@ -11,6 +11,8 @@
 #       sq        SQ / GRBM counter passes over tools/bench_legs/ops_pmc_leg.py
 #       evidence  round, then prof, then pmc (the end-of-round record for profiles/)
 #       leg       python tools/bench_legs/ARGS (one bench leg script)
+#       timeline  rocprofv3 kernel trace of tools/bench_legs/hist_leg.py ARGS (PHASES=0), last
+#                 TL_LAST (90) dispatches as a timeline
 # Every GPU step runs under its own time limit and the script stops at the first failure.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
@@ -70,6 +72,10 @@ case $M in
   pmc) run_pmc ;;
   sq) run_sq ;;
   evidence) run_tests; run_smoke; run_bench "$@"; run_prof; run_pmc ;;
+  timeline)  # kernel timeline of the last ~90 dispatches of a histogram leg: args go to hist_leg.py
+    (cd /tmp && export TMPDIR=/tmp PHASES=0 && timeout -k 10 600 rocprofv3 --kernel-trace --output-format rocpd -d $R/gpurun_out/${T}_kt -o run -- python3 $R/tools/bench_legs/hist_leg.py "$@" > $R/gpurun_out/${T}_kt.txt 2>&1) || { echo timeline_failed; tail -20 gpurun_out/${T}_kt.txt; exit 1; }
+    python tools/rocpd_timeline.py $(ls gpurun_out/${T}_kt/*.db gpurun_out/${T}_kt/*/*.db 2>/dev/null | head -1) ${TL_LAST:-90} > gpurun_out/${T}_timeline.txt
+    tail -4 gpurun_out/${T}_kt.txt; tail -45 gpurun_out/${T}_timeline.txt ;;
   leg)
     L=$1; shift
     timeout -k 10 900 python -u tools/bench_legs/$L "$@" > gpurun_out/${T}_leg.txt 2>&1 || { echo leg_failed; tail -30 gpurun_out/${T}_leg.txt; exit 1; }
