@@ -1030,7 +1030,35 @@ fphe_status launch_fold_segments(fphe_ctx* c, const u32* Src, const u8* ssign, c
   const size_t round = (size_t)occ_grid(c, ksf, lds, (size_t)1 << 40, "segfold") * kWavesPerBlock * E;
   size_t r = (T + round - 1) / round;
   r = r < 8 ? 8 : (r > (size_t)kSegFoldMax ? (size_t)kSegFoldMax : r);
-  const size_t nslots = (T + r - 1) / r;
+  size_t nslots = (T + r - 1) / r;
+  // raised keys (group_dev.h k_gr_gapsel / k_gr_plan): keys >= 8 exponents above their
+  // segment's least one get slots of their own whose partials k_segfold27 raises in place.
+  // FPHE_FOLD_RAISE=0 turns it off, =force raises every key above the least (tests).
+  const char* rmode = getenv("FPHE_FOLD_RAISE");
+  const bool rforce = rmode && !strcmp(rmode, "force");
+  const bool raise = NE > 1 && lds_counts && !(rmode && !strcmp(rmode, "0"));
+  int32_t* plan = nullptr;
+  u8* raised = nullptr;
+  if (raise) {
+    const size_t smax = 2 * std::max(round, nslots) + 2 * (size_t)kRaiseMax + 2;
+    if (smax < ((size_t)1 << 31)) {
+      int32_t* ng = B.get<int32_t>(1);
+      int32_t* gk = B.get<int32_t>(5 * (size_t)kRaiseMax);
+      plan = B.get<int32_t>(kPlanWords);
+      raised = B.get<u8>(nkeys);
+      if (!B.ok) return FPHE_ERR_HIP;
+      if (hipMemsetAsync(ng, 0, 4, s) != hipSuccess || hipMemsetAsync(raised, 0, nkeys, s) != hipSuccess)
+        return FPHE_ERR_HIP;
+      const int32_t gmin = rforce ? 1 : 8, xmax = rforce ? kI32Max : (int32_t)(r - 1);
+      hipLaunchKernelGGL(k_gr_gapsel, dim3(gr_grid(nseg, c->cus)), dim3(kGrBlock), 0, s, cntR, offR, nseg, (int32_t)NE,
+                         h[0], gmin, xmax, ng, gk, gk + kRaiseMax, gk + 2 * kRaiseMax, gk + 3 * kRaiseMax,
+                         gk + 4 * kRaiseMax);
+      hipLaunchKernelGGL(k_gr_plan, dim3(1), dim3(kGrBlock), 0, s, ng, gk, gk + kRaiseMax, gk + 2 * kRaiseMax,
+                         gk + 3 * kRaiseMax, gk + 4 * kRaiseMax, (int64_t)T, (int32_t)round, (int32_t)r,
+                         (int32_t)kSegFoldMax, (int32_t)smax, plan, raised);
+      nslots = smax;  // a bound: the plan's count is on the device (slots past it stay empty)
+    }
+  }
   int32_t* pcnt = B.get<int32_t>(nslots);
   int32_t* poff = B.get<int32_t>(nslots);
   int32_t* cnt2 = B.get<int32_t>(nkeys);
@@ -1038,9 +1066,11 @@ fphe_status launch_fold_segments(fphe_ctx* c, const u32* Src, const u8* ssign, c
   int32_t* tmp = B.get<int32_t>(nkeys);
   int32_t* hdr = B.get<int32_t>(4);
   if (!B.ok) return FPHE_ERR_HIP;
-  if (hipMemsetAsync(cnt2, 0, nkeys * 4, s) != hipSuccess || hipMemsetAsync(hdr, 0, 16, s) != hipSuccess)
+  if (hipMemsetAsync(cnt2, 0, nkeys * 4, s) != hipSuccess || hipMemsetAsync(hdr, 0, 16, s) != hipSuccess ||
+      (plan && hipMemsetAsync(pcnt, 0, nslots * 4, s) != hipSuccess))
     return FPHE_ERR_HIP;
-  hipLaunchKernelGGL(k_gr_segcount, dim3(gr_grid(nslots, c->cus)), dim3(kGrBlock), 0, s, skey, T, (u32)r, pcnt, cnt2);
+  hipLaunchKernelGGL(k_gr_segcount, dim3(gr_grid(nslots, c->cus)), dim3(kGrBlock), 0, s, skey, T, (u32)r,
+                     (const int32_t*)plan, pcnt, cnt2);
   if (dev_scan(c, pcnt, nslots, poff, hdr + 2, B) != FPHE_OK || dev_scan(c, cnt2, nkeys, off2, nullptr, B) != FPHE_OK)
     return FPHE_ERR_HIP;
   hipLaunchKernelGGL(k_gr_nchunks, dim3(gr_grid(nkeys, c->cus)), dim3(kGrBlock), 0, s, cnt2, nkeys, 1, tmp, hdr);
@@ -1055,7 +1085,8 @@ fphe_status launch_fold_segments(fphe_ctx* c, const u32* Src, const u8* ssign, c
   P.key = B.get<int32_t>(ub1);
   if (!B.ok || sj.join() != FPHE_OK) return FPHE_ERR_HIP;
   hipLaunchKernelGGL(ksf, dim3(occ_grid(c, ksf, lds, (nslots + E - 1) / E, "segfold")), dim3(kBlock), lds, s, c->K,
-                     rows, ssign, sexp, ord, skey, T, (u32)r, poff, P.rows, P.sign, P.exp, P.key, (u32)NL);
+                     rows, ssign, sexp, ord, skey, T, (u32)r, (const int32_t*)plan, poff, P.rows, P.sign, P.exp, P.key,
+                     (u32)NL);
   P.cnt = cnt2;
   P.off = off2;
   P.n_dev = hdr + 2;
@@ -1083,9 +1114,9 @@ fphe_status launch_fold_segments(fphe_ctx* c, const u32* Src, const u8* ssign, c
       return FPHE_ERR_HIP;
     const unsigned gp = gr_grid(np, c->cus);
     hipLaunchKernelGGL(k_gr_segmin<L>, dim3(gp), dim3(kGrBlock), 0, s, P.rows, P.sign, P.exp, P.key, P.n_dev,
-                       (int32_t)NE, c->K.N2M1, segmin, lit);
-    hipLaunchKernelGGL(k_gr_gaps, dim3(gp), dim3(kGrBlock), 0, s, P.exp, P.key, lit, P.n_dev, (int32_t)NE, segmin, gap,
-                       skey, scnt, gh, err);
+                       (int32_t)NE, c->K.N2M1, (const u8*)raised, segmin, lit);
+    hipLaunchKernelGGL(k_gr_gaps, dim3(gp), dim3(kGrBlock), 0, s, P.exp, P.key, lit, (const u8*)raised, P.n_dev,
+                       (int32_t)NE, segmin, gap, skey, scnt, gh, err);
     // partials in descending-gap order (counting sort on NE - 1 - gap: every gap < NE), then
     // the alignment; waves whose partials all have gap 0 skip their tile at once
     const size_t ng = (size_t)NE;

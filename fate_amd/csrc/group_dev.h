@@ -324,14 +324,21 @@ __global__ __launch_bounds__(kGrBlock) void k_gr_perm(const int32_t* __restrict_
   }
 }
 
-// The balanced first level's bookkeeping: slot i covers sorted items [i r, min((i+1) r, T));
+// The balanced first level's bookkeeping: slot i covers sorted items [i r, min((i+1) r, T)),
+// or the plan's range (slot_items);
 // pcnt[i] = partials it emits (1 + run changes inside its range), cnt2[key] += 1 per run
 // piece (the next level's per-key item counts).
 __global__ __launch_bounds__(kGrBlock) void k_gr_segcount(const int32_t* __restrict__ skey, size_t T, u32 r,
-                                                          int32_t* __restrict__ pcnt, int32_t* __restrict__ cnt2) {
-  const size_t nslots = (T + r - 1) / r;
+                                                          const int32_t* __restrict__ plan, int32_t* __restrict__ pcnt,
+                                                          int32_t* __restrict__ cnt2) {
+  const size_t nslots = plan ? (size_t)plan[1] : (T + r - 1) / r;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nslots; i += (size_t)gridDim.x * blockDim.x) {
-    const size_t p0 = i * r, p1 = p0 + r < T ? p0 + r : T;
+    size_t p0, p1;
+    slot_items(plan, i, T, r, p0, p1);
+    if (p1 <= p0) {  // a plan's padding slot: no items, no partial
+      pcnt[i] = 0;
+      continue;
+    }
     int32_t k = skey[p0], np = 1;
     for (size_t p = p0 + 1; p < p1; ++p) {
       const int32_t kp = skey[p];
@@ -368,11 +375,14 @@ __global__ __launch_bounds__(kGrBlock) void k_gr_chunks(const int32_t* __restric
 // reference's zero: signed integer exactly 1, stored as M(1) = `one`) and the segment's least
 // non-literal exponent.
 template <int L>
+// raised (may be null, per key): partials k_segfold27 already raised to an exponent chosen
+// before the segment's least exponent was known -- they stay out of that minimum (k_gr_gaps
+// checks the choice)
 __global__ __launch_bounds__(kGrBlock) void k_gr_segmin(const u32* __restrict__ rows, const u8* __restrict__ sign,
                                                         const int32_t* __restrict__ exp, const int32_t* __restrict__ pkey,
                                                         const int32_t* __restrict__ np_dev, int32_t NE,
-                                                        const u32* __restrict__ one, int32_t* __restrict__ segmin,
-                                                        u8* __restrict__ lit) {
+                                                        const u32* __restrict__ one, const u8* __restrict__ raised,
+                                                        int32_t* __restrict__ segmin, u8* __restrict__ lit) {
   const int32_t np = *np_dev;
   for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < (size_t)np; p += (size_t)gridDim.x * blockDim.x) {
     const u32* r = rows + p * L;
@@ -380,15 +390,20 @@ __global__ __launch_bounds__(kGrBlock) void k_gr_segmin(const u32* __restrict__ 
     for (int j = 0; j < L; ++j) acc |= r[j] ^ one[j];
     const bool one = acc == 0 && sign[p] == 0;
     lit[p] = one ? 1 : 0;
-    if (!one) atomicMin(&segmin[pkey[p] / NE], exp[p]);
+    if (!one && !(raised && raised[pkey[p]])) atomicMin(&segmin[pkey[p] / NE], exp[p]);
   }
 }
 
 // gap[p] = exp - segmin (0 for literal partials and all-literal segments), exp[p] = segmin (the
 // exponent every partial of the segment is aligned to), nseg-keys for the next fold, counts;
 // gap beyond kMaxGap -> err (fphe_align's contract).  gmax = the largest gap (device).
+// A raised partial (non-literal) must sit at or above the least exponent of the segment's
+// other partials: otherwise the exponent it was raised to was below the reference's (the
+// segment's least key held only literal 1s), and the call reports FPHE_EF_EXP_RANGE -- the
+// caller then folds without the device merge (paillier._fold_dense), exactly.
 __global__ __launch_bounds__(kGrBlock) void k_gr_gaps(int32_t* __restrict__ exp, const int32_t* __restrict__ pkey,
-                                                      const u8* __restrict__ lit, const int32_t* __restrict__ np_dev,
+                                                      const u8* __restrict__ lit, const u8* __restrict__ raised,
+                                                      const int32_t* __restrict__ np_dev,
                                                       int32_t NE, const int32_t* __restrict__ segmin,
                                                       int32_t* __restrict__ gap, int32_t* __restrict__ skey,
                                                       int32_t* __restrict__ scnt, int32_t* __restrict__ gmax,
@@ -399,6 +414,7 @@ __global__ __launch_bounds__(kGrBlock) void k_gr_gaps(int32_t* __restrict__ exp,
     const int32_t s = pkey[p] / NE;
     const int32_t m = segmin[s];
     int32_t d = 0;
+    if (raised && raised[pkey[p]] && !lit[p] && (m == kI32Max || exp[p] < m)) ef |= FPHE_EF_EXP_RANGE;
     if (m != kI32Max) {
       if (!lit[p]) {
         const long long dd = (long long)exp[p] - m;
@@ -413,6 +429,158 @@ __global__ __launch_bounds__(kGrBlock) void k_gr_gaps(int32_t* __restrict__ exp,
     if (d) atomicMax(gmax, d);
   }
   set_err(err, ef);
+}
+
+// --- raised keys and the slot plan (fphe_fold_segments; kernels27.h kRaiseMax) ---------------
+// A (segment, exponent) key far above its segment's least exponent -- the reference's rare
+// outliers, e.g. +-1e-30 or +-3.4e38 among gradients near 1 -- would need 4 gap squarings of its
+// partial in the exponent merge, on one wave after the whole fold.  Raised keys get slots of
+// their own in k_segfold27, which squares their partials there.  Per segment (one thread):
+// every key >= gmin exponents above the segment's least key exponent (jmin) is raised to it, if
+// raise_cost(gap) (its 4 gap squarings, in products) is at most xmax.  The least key may turn out to hold only
+// literal 1s; k_gr_gaps then reports it and the caller folds without the device merge.
+__global__ __launch_bounds__(kGrBlock) void k_gr_gapsel(const int32_t* __restrict__ cnt, const int32_t* __restrict__ off,
+                                                        size_t nseg, int32_t NE, int32_t emin, int32_t gmin, int32_t xmax,
+                                                        int32_t* __restrict__ ng, int32_t* __restrict__ gkey,
+                                                        int32_t* __restrict__ gcnt, int32_t* __restrict__ goff,
+                                                        int32_t* __restrict__ ggap, int32_t* __restrict__ gexp) {
+  for (size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x; s < nseg; s += (size_t)gridDim.x * blockDim.x) {
+    const int32_t* c = cnt + s * NE;
+    int32_t jmin = 0;
+    while (jmin < NE && c[jmin] == 0) ++jmin;
+    for (int32_t j = jmin + gmin; j < NE; ++j) {
+      if (c[j] == 0 || raise_cost(j - jmin) > xmax) continue;
+      const int32_t h = atomicAdd(ng, 1);
+      if (h >= kRaiseMax) return;
+      const int32_t k = (int32_t)(s * NE) + j;
+      gkey[h] = k;
+      gcnt[h] = c[j];
+      goff[h] = off[k];
+      ggap[h] = j - jmin;
+      gexp[h] = emin + jmin;
+    }
+  }
+}
+
+// One workgroup: the slot plan (kernels27.h) for the raised keys k_gr_gapsel found.  Regions in
+// item order: stretch, raised key, stretch, ..., stretch.  A region of n items takes
+// ceil(n / cap) slots, cap = r for a stretch and max(1, r - raise_cost(gap)) for a raised key,
+// its items spread evenly over them (a raised slot's squarings are products in the same loop,
+// so a wave mixing regions costs its longest lane, no more).  r is the least value in
+// [r0, rmax] whose plan fits one round of `round` slots (rmax when none does: a multi-round
+// launch).  A plan over `smax` slots falls back to the uniform one (no raised keys).
+// raised[key] = 1 for the keys the plan raises.
+__global__ __launch_bounds__(kGrBlock) void k_gr_plan(const int32_t* __restrict__ ng_dev, const int32_t* __restrict__ gkey,
+                                                      const int32_t* __restrict__ gcnt, const int32_t* __restrict__ goff,
+                                                      const int32_t* __restrict__ ggap, const int32_t* __restrict__ gexp,
+                                                      int64_t T, int32_t round, int32_t r0, int32_t rmax, int32_t smax,
+                                                      int32_t* __restrict__ plan, u8* __restrict__ raised) {
+  __shared__ int32_t sk[kRaiseMax], sc[kRaiseMax], so[kRaiseMax], sg[kRaiseMax], se[kRaiseMax];
+  __shared__ int64_t part[kGrBlock];
+  __shared__ int32_t use_r;
+  const int t = threadIdx.x;
+  __shared__ int32_t kin[kRaiseMax];
+  int32_t ng = *ng_dev;
+  ng = ng < kRaiseMax ? ng : kRaiseMax;
+  for (int i = t; i < ng; i += kGrBlock) kin[i] = gkey[i];
+  __syncthreads();
+  // rank sort by key (keys are distinct)
+  for (int i = t; i < ng; i += kGrBlock) {
+    const int32_t k = kin[i];
+    int rk = 0;
+    for (int j = 0; j < ng; ++j) rk += kin[j] < k;
+    sk[rk] = k;
+    sc[rk] = gcnt[i];
+    so[rk] = goff[i];
+    sg[rk] = ggap[i];
+    se[rk] = gexp[i];
+  }
+  __syncthreads();
+  const int nreg = 2 * ng + 1;
+  auto reg = [&](int i, int64_t& st, int64_t& en, int& g) {  // region i's items and gap
+    if (i & 1) {
+      const int h = i >> 1;
+      st = so[h];
+      en = (int64_t)so[h] + sc[h];
+      g = sg[h];
+    } else {
+      const int h = i >> 1;
+      st = h == 0 ? 0 : (int64_t)so[h - 1] + sc[h - 1];
+      en = h == ng ? T : (int64_t)so[h];
+      g = 0;
+    }
+  };
+  auto reg_slots = [&](int i, int64_t r, int64_t& per) -> int64_t {
+    int64_t st, en;
+    int g;
+    reg(i, st, en, g);
+    const int64_t n = en - st;
+    if (n <= 0) {
+      per = 1;
+      return 0;
+    }
+    const int64_t x = g ? raise_cost(g) : 0;
+    const int64_t cap = r - x > 1 ? r - x : 1;
+    const int64_t ns = (n + cap - 1) / cap;
+    per = (n + ns - 1) / ns;
+    return ns;
+  };
+  auto total = [&](int64_t r) -> int64_t {  // block-wide sum of the regions' slots
+    int64_t s = 0, per;
+    for (int i = t; i < nreg; i += kGrBlock) s += reg_slots(i, r, per);
+    part[t] = s;
+    __syncthreads();
+    for (int o = kGrBlock / 2; o > 0; o >>= 1) {
+      if (t < o) part[t] += part[t + o];
+      __syncthreads();
+    }
+    const int64_t v = part[0];
+    __syncthreads();
+    return v;
+  };
+  int64_t lo = r0, hi = rmax;
+  if (total(rmax) > round) lo = hi = rmax;
+  while (lo < hi) {  // least r with total(r) <= round (total is non-increasing in r)
+    const int64_t mid = (lo + hi) / 2;
+    if (total(mid) <= round) hi = mid;
+    else lo = mid + 1;
+  }
+  const int64_t S = ng ? total(lo) : 0;
+  if (t == 0) use_r = (ng == 0 || S > smax) ? -1 : (int32_t)lo;
+  __syncthreads();
+  int32_t* rslot = plan + 2;
+  if (use_r < 0) {  // the uniform plan: one stretch at r0 items per slot
+    if (t == 0) {
+      plan[0] = 1;
+      plan[1] = (int32_t)((T + r0 - 1) / r0);
+      rslot[0] = 0;
+      rslot[kPlanRegions] = 0;
+      rslot[2 * kPlanRegions] = (int32_t)T;
+      rslot[3 * kPlanRegions] = r0;
+      rslot[4 * kPlanRegions] = 0;
+      rslot[5 * kPlanRegions] = 0;
+    }
+    return;
+  }
+  for (int h = t; h < ng; h += kGrBlock) raised[sk[h]] = 1;
+  if (t == 0) {  // the regions' first slots: a serial scan over <= kPlanRegions entries
+    int64_t acc = 0, per;
+    for (int i = 0; i < nreg; ++i) {
+      int64_t st, en;
+      int g;
+      reg(i, st, en, g);
+      const int64_t ns = reg_slots(i, use_r, per);
+      rslot[i] = (int32_t)acc;
+      rslot[kPlanRegions + i] = (int32_t)st;
+      rslot[2 * kPlanRegions + i] = (int32_t)(en > st ? en : st);
+      rslot[3 * kPlanRegions + i] = (int32_t)per;
+      rslot[4 * kPlanRegions + i] = g;
+      rslot[5 * kPlanRegions + i] = (i & 1) ? se[i >> 1] : 0;
+      acc += ns;
+    }
+    plan[0] = nreg;
+    plan[1] = (int32_t)acc;
+  }
 }
 
 // counting-sort keys for the descending-gap order of the alignment: key = gmax - gap (n on

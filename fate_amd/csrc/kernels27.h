@@ -107,6 +107,59 @@ __device__ __forceinline__ ColIO colio(const u32* tile_base, u32 rows, u32 col, 
 constexpr int kFoldMax = 64;  // terms per k_fold27 chunk
 // items per wave slot of the balanced first fold level (k_segfold27), at most
 constexpr int kSegFoldMax = 1024;
+// Slot plan of the balanced first fold level (fphe_fold_segments, group_dev.h k_gr_plan):
+// the sorted items cut into regions -- stretches packed at `rlen` items per wave slot, and the
+// runs of "raised" keys (far above their segment's least exponent), each cut into slots of
+// fewer items so that a slot's products plus its closing 4 gap squarings take about as long as
+// a stretch slot.  k_segfold27 raises such a slot's partial to the segment's least exponent
+// itself, inside the balanced launch, instead of leaving a 4-gap-squaring chain on one wave
+// after it (the exponent merge).  One int32 buffer:
+//   [0] regions, [1] slots, then kPlanRegions entries each of rslot (first slot; rslot of the
+//   last region + its slots = total), rstart, rend (items), rlen (items per slot), rgap, rexp.
+constexpr int kRaiseMax = 256;                     // raised keys per call, at most
+constexpr int kPlanRegions = 2 * kRaiseMax + 1;
+constexpr int kPlanWords = 2 + 6 * kPlanRegions;
+// the slot-plan weight of raising a partial by 16^gap: 4 gap squarings, each a product of the
+// partial with itself in k_segfold27's loop
+__host__ __device__ constexpr long long raise_cost(long long gap) { return 4 * gap; }
+struct SlotRange {
+  int64_t p0, p1;  // items [p0, p1)
+  int gap;         // raise the slot's partial by 16^gap (0: a stretch slot)
+  int ex;          // ... to this exponent
+};
+__device__ __forceinline__ SlotRange plan_range(const int32_t* __restrict__ plan, size_t slot) {
+  const int32_t nreg = plan[0];
+  const int32_t* rslot = plan + 2;
+  int lo = 0, hi = nreg - 1;  // the last region whose first slot is <= slot
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if ((size_t)rslot[mid] <= slot) lo = mid;
+    else hi = mid - 1;
+  }
+  const int32_t* f = plan + 2 + lo;
+  SlotRange s;
+  const int64_t len = f[3 * kPlanRegions], end = f[2 * kPlanRegions];
+  s.p0 = (int64_t)f[kPlanRegions] + (int64_t)(slot - (size_t)f[0]) * len;
+  s.p0 = s.p0 < end ? s.p0 : end;  // a region's padding slots are empty
+  s.p1 = s.p0 + len < end ? s.p0 + len : end;
+  s.gap = f[4 * kPlanRegions];
+  s.ex = f[5 * kPlanRegions];
+  return s;
+}
+
+// slot -> items: the plan's, or i r .. (i + 1) r without one
+__device__ __forceinline__ void slot_items(const int32_t* __restrict__ plan, size_t i, size_t T, uint32_t r, size_t& p0,
+                                           size_t& p1) {
+  if (plan) {
+    const SlotRange sr = plan_range(plan, i);
+    p0 = (size_t)sr.p0;
+    p1 = (size_t)sr.p1;
+  } else {
+    p0 = i * r;
+    p1 = p0 + r < T ? p0 + r : T;
+  }
+}
+
 // largest exponent gap k_add27 / k_align27 act on (4 kMaxGap squarings, ~7 s on one wave):
 // far beyond the reference encoders' exponent range (f64: [-282, 242]); fphe_align rejects
 // larger gaps on the host side (fate_amd/paillier.py), k_add27 caps them

@@ -191,3 +191,49 @@ def test_iupdate_position_range_checked_before_narrowing(env):
     for bad in ([[0], [(1 << 32) + 1]], torch.tensor([[0], [(1 << 32) + 1]]), torch.tensor([[0], [-1]])):
         with pytest.raises(P.PanicException):
             hist.iupdate(v, bad, 1, pk)
+
+
+def test_fold_raised_keys_forced(env, monkeypatch):
+    """FPHE_FOLD_RAISE=force: every key above its segment's least exponent gets its own slots
+    and k_segfold27 raises its partial in place (the slot plan of k_gr_plan), against the
+    oracle -- wide exponents, literal 1s (a segment whose least key holds only literals makes
+    the device report it, and the call folds without the device merge), empty segments."""
+    fx, sk, pk, coder, opk, cts = env
+    rng = random.Random(23)
+    src = mixed_sources(opk, cts, 160, 23)
+    nseg = 17
+    T = 900
+    idx = [rng.randrange(len(src)) for _ in range(T)]
+    seg = [rng.randrange(nseg - 2) for _ in range(T)]
+    lits = [i for i, c in enumerate(src) if c.c == 1]
+    low = min(range(len(src)), key=lambda i: src[i].exp if src[i].c != 1 else 99)
+    idx += [lits[0], lits[1], low]  # segment nseg-2: a literal below a real term far above it
+    seg += [nseg - 2] * 3
+    want = oracle_fold(opk, src, idx, seg, nseg)
+    monkeypatch.setenv("FPHE_FOLD_RAISE", "force")
+    got = P._fold_to_segments(pk, dev_vec(pk, src), torch.tensor(seg), nseg, index=torch.tensor(idx))
+    assert host(pk, got) == want
+
+
+@pytest.mark.parametrize("bits", [2048])
+def test_fold_raised_keys_auto_matches_merge(bits, monkeypatch):
+    """The automatic raise (keys >= 8 exponents above their segment's least, at a size where
+    the balanced level has room for their squarings: 2.1M terms) returns the same integers as
+    the plain exponent merge (FPHE_FOLD_RAISE=0), with outliers 9 and 10 exponents above and
+    below the bulk of their segments."""
+    fx, sk, pk, coder, opk, cts = load(bits)
+    base = more(opk, cts, 512, 31)
+    rng = random.Random(31)
+    exps = [-13] * 512
+    for i in range(0, 512, 37):
+        exps[i] = -13 + rng.choice([9, 10, -9, -10])
+    src = [O.Ciphertext(c.c, e) for c, e in zip(base, exps)]
+    v = dev_vec(pk, src)
+    g = torch.Generator().manual_seed(31)
+    T = 2_100_000
+    idx = torch.randint(0, 512, (T,), generator=g)
+    seg = torch.randint(0, 64, (T,), generator=g)
+    got = host(pk, P._fold_to_segments(pk, v, seg, 64, index=idx))
+    monkeypatch.setenv("FPHE_FOLD_RAISE", "0")
+    want = host(pk, P._fold_to_segments(pk, v, seg, 64, index=idx))
+    assert got == want

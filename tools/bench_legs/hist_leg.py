@@ -67,6 +67,16 @@ def timed(name):
 if os.environ.get("PHASES", "1") != "0":
     for name in orig:
         setattr(P, name, timed(name))
+BURST = int(os.environ.get("HIST_BURST", "1"))
+if BURST > 1:  # k iupdates queued back to back (no host sync between): the GPU stays busy
+    hs = [P.CiphertextVector.zeros(HF * NB * 2, pk._key.L2, dev) for _ in range(BURST)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for h in hs:
+        h.iupdate(gh, positions, 2, pk)
+    torch.cuda.synchronize()
+    tot = time.perf_counter() - t0
+    print(json.dumps({"burst": BURST, "total_s": round(tot, 4), "per_call_s": round(tot / BURST, 5)}), flush=True)
 for rep in range(2):
     T.clear()
     hist = P.CiphertextVector.zeros(HF * NB * 2, pk._key.L2, dev)

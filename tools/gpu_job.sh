@@ -1,7 +1,8 @@
 # Parameterised GPU job (replaces rounds 1-3's fifty one-off tools/gpu_job_*.sh scripts;
 # same-box A/B of library variants stays in tools/gpu_job_ab.sh).
 #   bash tools/gpu_job.sh TAG MODE [args...]
-# MODE  tests     the GPU test suite (no -x: every failure listed); args select tests
+# MODE  tests     the GPU test suite (no -x: every failure listed); args: test files / -k filters
+#                 in place of the whole tests/ directory
 #       round     tests + smoke + the default bench line (args go to bench.py)
 #       bench     the default bench line only (args go to bench.py)
 #       prof      rocprofv3 --kernel-trace --stats of a short bench run
@@ -23,7 +24,9 @@ cd $R
 mkdir -p gpurun_out
 
 run_tests() {
-  timeout -k 10 1200 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread "$@" > gpurun_out/${T}_tests.txt 2>&1
+  local sel=("$@")
+  [ ${#sel[@]} -eq 0 ] && sel=(tests)
+  timeout -k 10 1200 python -u -m pytest "${sel[@]}" -m gpu -v --timeout 300 --timeout-method thread > gpurun_out/${T}_tests.txt 2>&1
   local rc=$?
   grep -E "passed|failed|error" gpurun_out/${T}_tests.txt | tail -3
   grep -E "^FAILED|^ERROR" gpurun_out/${T}_tests.txt | head -40
@@ -71,6 +74,21 @@ case $M in
   prof) run_prof "$@" ;;
   pmc) run_pmc ;;
   sq) run_sq ;;
+  sqhist)  # SQ / GRBM counters over tools/bench_legs/hist_leg.py ARGS (PHASES=0)
+    export PHASES=0
+    pmc_pass sqh "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE GRBM_COUNT" python3 $R/tools/bench_legs/hist_leg.py "$@"
+    python3 - gpurun_out/${T}_sqh <<'PYEOF'
+import csv, glob, sys, collections
+agg = collections.defaultdict(dict)
+for f in glob.glob(sys.argv[1] + "/**/run_counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        if "segfold" in r["Kernel_Name"] or "align_rows" in r["Kernel_Name"]:
+            k = (r["Kernel_Name"].split("(")[0][-40:], int(r["Dispatch_Id"]))
+            agg[k][r["Counter_Name"]] = agg[k].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+for k, v in sorted(agg.items(), key=lambda kv: kv[0][1]):
+    print(k, {c: round(x) for c, x in sorted(v.items())})
+PYEOF
+    ;;
   evidence) run_tests; run_smoke; run_bench "$@"; run_prof; run_pmc ;;
   timeline)  # kernel timeline of the last ~90 dispatches of a histogram leg: args go to hist_leg.py
     (cd /tmp && export TMPDIR=/tmp PHASES=0 && timeout -k 10 600 rocprofv3 --kernel-trace --output-format rocpd -d $R/gpurun_out/${T}_kt -o run -- python3 $R/tools/bench_legs/hist_leg.py "$@" > $R/gpurun_out/${T}_kt.txt 2>&1) || { echo timeline_failed; tail -20 gpurun_out/${T}_kt.txt; exit 1; }
