@@ -686,9 +686,22 @@ def main() -> None:
         # 124-squaring alignment chain, a ~4.8 ms critical path on a single wave
         gh_edge = P.Evaluator.cat([ct, ct2])._gather(torch.stack([torch.arange(N), N + torch.arange(N)], 1).reshape(-1))
         he, hist_edge_s, hist_edge_ok, _ = run_hist(gh_edge, x.double(), torch.flip(x, [0]).double() * 0.25)
+        # the same data without the edge values (their 8 samples' g, and the 8 mirrored h, are
+        # replaced by copies of neighbouring elements): what the edge values alone cost
+        sel = torch.arange(2 * N)
+        sel[0:16:2] = torch.arange(16, 32, 2)
+        sel[2 * N - 15::2] = torch.arange(2 * N - 31, 2 * N - 15, 2)
+        gh_ne = gh_edge._gather(sel)
+        wg_ne, wh_ne = x.double().clone(), torch.flip(x, [0]).double() * 0.25
+        wg_ne[:8] = wg_ne[8:16].clone()
+        wh_ne[N - 8:] = wh_ne[N - 16:N - 8].clone()
+        hne, hist_ne_s, hist_ne_ok, _ = run_hist(gh_ne, wg_ne, wh_ne)
         hist_edge = {"iupdate_s": round(hist_edge_s, 5), "allclose": hist_edge_ok,
-                     "roofline_frac": iupdate_roofline(gh_edge, positions, 2, HF * NB * 2, hist_edge_s, key_bits)["frac"]}
-        del he, gh_edge
+                     "roofline_frac": iupdate_roofline(gh_edge, positions, 2, HF * NB * 2, hist_edge_s, key_bits)["frac"],
+                     "iupdate_s_same_data_without_edge_values": round(hist_ne_s, 5),
+                     "allclose_without_edge_values": hist_ne_ok,
+                     "edge_over_without": round(hist_edge_s / hist_ne_s, 3)}
+        del he, gh_edge, hne, gh_ne
         hist_mgpu = None
         if dist:
             # config 4 across GPUs: each rank folded its own samples; the

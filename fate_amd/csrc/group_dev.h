@@ -563,23 +563,38 @@ __global__ __launch_bounds__(kGrBlock) void k_gr_plan(const int32_t* __restrict_
     return;
   }
   for (int h = t; h < ng; h += kGrBlock) raised[sk[h]] = 1;
-  if (t == 0) {  // the regions' first slots: a serial scan over <= kPlanRegions entries
-    int64_t acc = 0, per;
-    for (int i = 0; i < nreg; ++i) {
-      int64_t st, en;
-      int g;
-      reg(i, st, en, g);
-      const int64_t ns = reg_slots(i, use_r, per);
-      rslot[i] = (int32_t)acc;
-      rslot[kPlanRegions + i] = (int32_t)st;
-      rslot[2 * kPlanRegions + i] = (int32_t)(en > st ? en : st);
-      rslot[3 * kPlanRegions + i] = (int32_t)per;
-      rslot[4 * kPlanRegions + i] = g;
-      rslot[5 * kPlanRegions + i] = (i & 1) ? se[i >> 1] : 0;
-      acc += ns;
+  // the regions' first slots: each thread a contiguous piece of the regions, then a scan of
+  // the pieces' totals (64-bit divisions stay out of any serial loop)
+  const int piece = (nreg + kGrBlock - 1) / kGrBlock;
+  const int i0 = t * piece, i1 = i0 + piece < nreg ? i0 + piece : nreg;
+  int64_t mine = 0, per;
+  for (int i = i0; i < i1; ++i) mine += reg_slots(i, use_r, per);
+  part[t] = mine;
+  __syncthreads();
+  if (t == 0) {
+    int64_t acc = 0;
+    for (int u = 0; u < kGrBlock; ++u) {
+      const int64_t v = part[u];
+      part[u] = acc;
+      acc += v;
     }
     plan[0] = nreg;
     plan[1] = (int32_t)acc;
+  }
+  __syncthreads();
+  int64_t acc = part[t];
+  for (int i = i0; i < i1; ++i) {
+    int64_t st, en;
+    int g;
+    reg(i, st, en, g);
+    const int64_t ns = reg_slots(i, use_r, per);
+    rslot[i] = (int32_t)acc;
+    rslot[kPlanRegions + i] = (int32_t)st;
+    rslot[2 * kPlanRegions + i] = (int32_t)(en > st ? en : st);
+    rslot[3 * kPlanRegions + i] = (int32_t)per;
+    rslot[4 * kPlanRegions + i] = g;
+    rslot[5 * kPlanRegions + i] = (i & 1) ? se[i >> 1] : 0;
+    acc += ns;
   }
 }
 

@@ -116,7 +116,7 @@ constexpr int kSegFoldMax = 1024;
 // after it (the exponent merge).  One int32 buffer:
 //   [0] regions, [1] slots, then kPlanRegions entries each of rslot (first slot; rslot of the
 //   last region + its slots = total), rstart, rend (items), rlen (items per slot), rgap, rexp.
-constexpr int kRaiseMax = 256;                     // raised keys per call, at most
+constexpr int kRaiseMax = 512;                     // raised keys per call, at most
 constexpr int kPlanRegions = 2 * kRaiseMax + 1;
 constexpr int kPlanWords = 2 + 6 * kPlanRegions;
 // the slot-plan weight of raising a partial by 16^gap: 4 gap squarings, each a product of the

@@ -93,7 +93,8 @@ PYEOF
   timeline)  # kernel timeline of the last ~90 dispatches of a histogram leg: args go to hist_leg.py
     (cd /tmp && export TMPDIR=/tmp PHASES=0 && timeout -k 10 600 rocprofv3 --kernel-trace --output-format rocpd -d $R/gpurun_out/${T}_kt -o run -- python3 $R/tools/bench_legs/hist_leg.py "$@" > $R/gpurun_out/${T}_kt.txt 2>&1) || { echo timeline_failed; tail -20 gpurun_out/${T}_kt.txt; exit 1; }
     python tools/rocpd_timeline.py $(ls gpurun_out/${T}_kt/*.db gpurun_out/${T}_kt/*/*.db 2>/dev/null | head -1) ${TL_LAST:-90} > gpurun_out/${T}_timeline.txt
-    tail -4 gpurun_out/${T}_kt.txt; tail -45 gpurun_out/${T}_timeline.txt ;;
+    rm -rf gpurun_out/${T}_kt  # the trace database: tens of MB, the timeline holds what is read
+    grep -E "total_s|burst" gpurun_out/${T}_kt.txt | tail -3; grep -E "segfold|align_rows|k_gr_plan|span" gpurun_out/${T}_timeline.txt ;;
   leg)
     L=$1; shift
     timeout -k 10 900 python -u tools/bench_legs/$L "$@" > gpurun_out/${T}_leg.txt 2>&1 || { echo leg_failed; tail -30 gpurun_out/${T}_leg.txt; exit 1; }
