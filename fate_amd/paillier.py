@@ -835,12 +835,16 @@ class CiphertextVector:
         slot = (pp[:, None] * stride + t).reshape(-1)
         # one ciphertext per slot (the literal 1 where no term lands: add's identity), then
         # data[s] = add(data[s], fold(terms of s)) for every slot at once
-        errs = []  # read back after the add is queued: the host work overlaps the fold's tail
-        folded, present = _fold_to_segments(pk, other, slot, self.count, index=src, with_present=True, deferred=errs)
+        # the error flags of the fold and of the add are read back once both are queued: no
+        # host sync between the launches
+        ferr, aerr = [], []
+        folded, present = _fold_to_segments(pk, other, slot, self.count, index=src, with_present=True, deferred=ferr)
         cur = _fit_limbs(self, pk._key.L2)
-        r = _add(pk, cur, folded, broadcast=False)
-        if _fold_failed(errs):  # an exponent gap beyond the device merge: the exact torch path
+        r = _add(pk, cur, folded, broadcast=False, deferred=aerr)
+        if _fold_failed(ferr):  # an exponent gap beyond the device merge: the exact torch path
             folded, present = _fold_dense(pk, other, slot, self.count, src)
+            r = _add(pk, cur, folded, broadcast=False)
+        elif _fold_failed(aerr):  # a gap beyond k_add27's range: pre-aligned, exact
             r = _add(pk, cur, folded, broadcast=False)
         # slots no term reaches keep their value as it was (exponent of a literal 1 included:
         # the reference never touches them)
@@ -1049,7 +1053,11 @@ def _prealign(pk: "PK", a: CiphertextVector, b: CiphertextVector, n: int
 
 
 def _add(pk: "PK", a: CiphertextVector, b: CiphertextVector, broadcast: bool, count: Optional[int] = None,
-         reorder: bool = True) -> CiphertextVector:
+         reorder: bool = True, deferred: Optional[list] = None) -> CiphertextVector:
+    """deferred: a list to append the kernel's device error flags to instead of checking the
+    gaps first (no read-back here); the caller tests them with :func:`_fold_failed` once its
+    later launches are queued and redoes the add without `deferred` if a gap was beyond
+    MAX_GAP (the flagged elements are unspecified)."""
     dev = a.device
     a, b = _fit_limbs(a, pk._key.L2), _fit_limbs(b, pk._key.L2)
     n = a.count if count is None else count
@@ -1058,12 +1066,17 @@ def _add(pk: "PK", a: CiphertextVector, b: CiphertextVector, broadcast: bool, co
     out = CiphertextVector.empty(n, a.L2, dev)
     if n == 0:
         return out
-    # the kernel is exact for exponent gaps up to MAX_GAP (one read-back of the largest gap)
-    eb = b.exp[:1].expand(n) if broadcast else b.exp[:n]
-    if int((a.exp[:n].to(torch.int64) - eb.to(torch.int64)).abs().max()) > MAX_GAP:
-        if broadcast:
-            b, broadcast = b._gather(torch.zeros(n, dtype=torch.long)), False
-        a, b = _prealign(pk, a, b, n)
+    err = None
+    if deferred is not None:
+        err = torch.zeros(1, dtype=torch.int32, device=dev)
+        deferred.append(err)
+    else:
+        # the kernel is exact for exponent gaps up to MAX_GAP (one read-back of the largest gap)
+        eb = b.exp[:1].expand(n) if broadcast else b.exp[:n]
+        if int((a.exp[:n].to(torch.int64) - eb.to(torch.int64)).abs().max()) > MAX_GAP:
+            if broadcast:
+                b, broadcast = b._gather(torch.zeros(n, dtype=torch.long)), False
+            a, b = _prealign(pk, a, b, n)
     lib = _lib.load()
     ctx = pk._key.ctx(dev)
     stream = ctypes.c_void_p(_stream(dev))
@@ -1077,7 +1090,8 @@ def _add(pk: "PK", a: CiphertextVector, b: CiphertextVector, broadcast: bool, co
         bC, bs, be = (b.C, b.sign, b.exp) if broadcast else (b.C[t0:t1], b.sign[e0:e1], b.exp[e0:e1])
         _lib.check(lib.fphe_add_ordered(ctx, _ptr(a.C[t0:t1]), _ptr(a.sign[e0:e1]), _ptr(a.exp[e0:e1]), _ptr(bC),
                                         _ptr(bs), _ptr(be), 0 if broadcast else 1, m, _ptr(order),
-                                        _ptr(out.C[t0:t1]), _ptr(out.sign[e0:e1]), _ptr(out.exp[e0:e1]), None, stream),
+                                        _ptr(out.C[t0:t1]), _ptr(out.sign[e0:e1]), _ptr(out.exp[e0:e1]), _ptr(err),
+                                        stream),
                    "fphe_add_ordered")
         del order  # the launch is stream-ordered: the allocator reuses the block only after it
     return out

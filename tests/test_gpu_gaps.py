@@ -127,3 +127,21 @@ def test_wire_state_carries_extreme_exponents(k1024):
     state = wire.ciphertext_vector_to_bincode(v)
     back, used = wire.ciphertext_vector_from_bincode(state)
     assert used == len(state) and back.to_signed_ints() == (cs, [2 ** 31 - 1, -2 ** 31])
+
+
+def test_iupdate_exact_gap_between_histogram_and_terms(k1024):
+    """The histogram's own values sit 70,000 exponents away from the folded terms: iupdate's
+    final ct-add (queued without a gap read-back) flags it, and the add is redone pre-aligned
+    -- bit-exact with the reference's sequential iupdate."""
+    sk, pk, coder, osk, opk, _ = k1024
+    cs = _cts(opk, 4, 11)
+    hc = _cts(opk, 3, 12)
+    hexps = [70000, -70000, 1]
+    exps = [0, 0, 2, -1]
+    hist = _unpickled(pk, hc, hexps)
+    src = _unpickled(pk, cs, exps)
+    positions = [[0], [1], [2, 0], [1]]
+    hist.iupdate(src, positions, 1, pk)
+    want = [O.Ciphertext(c, e) for c, e in zip(hc, hexps)]
+    O.iupdate(opk, want, [O.Ciphertext(c, e) for c, e in zip(cs, exps)], positions, 1)
+    assert hist.to_signed_ints(pk.ns) == ([w.c for w in want], [w.exp for w in want])
