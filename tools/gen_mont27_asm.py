@@ -158,17 +158,22 @@ def gen(LL, LB):
         out.append("}")
     out.append("#elif RG_SECTION == 3")
     out.append("template <int TPI, int a> __device__ __forceinline__ void r27f_sqrow(u64 (&T)[LL], const L27& A, u32 bf, u32 bm, u32 bl, const Mod<TPI>& N, u32 np, u32 mk);")
-    tpis = ((4, "quad_perm:[0,0,0,0]", "RGF"), (2, "quad_perm:[0,0,2,2]", "RGF2"), (8, "quad_perm:[0,0,0,0]", "RGF8"))
+    # TPI 1 (one lane per element: p^2, q^2 and n of <= 1024-bit keys) runs the TPI-4 rows with
+    # an identity DPP for m (the lane is its element's lane 0) and the modulus limbs in SGPRs
+    # (wave-uniform); the X hand-off from the next lane is that element's lane-0 X, which is
+    # 0 mod 2^LB, so no select is needed there either
+    tpis = ((4, "quad_perm:[0,0,0,0]", "RGF", "v"), (2, "quad_perm:[0,0,2,2]", "RGF2", "v"),
+            (8, "quad_perm:[0,0,0,0]", "RGF8", "v"), (1, "quad_perm:[0,1,2,3]", "RGF", "s"))
     for a in range(LL):
-        for tpi, bc, fam in tpis:
+        for tpi, bc, fam, nc in tpis:
             out.append(f"template <> __device__ __forceinline__ void r27f_sqrow<{tpi}, {a}>(u64 (&T)[LL], const L27& A, u32 bf, u32 bm, u32 bl, const Mod<{tpi}>& N, u32 np, u32 mk) {{")
             bl_in = ' [bl] "v"(bl),' if LL % 2 == 0 else ''
-            out.append(f'  asm volatile({fam}_SQROW_{a}("{bc}") : RGF_T_OPS(T) : RG_A_INS(A), RG_N_INS(N, "v"), [bf] "v"(bf), [bm] "v"(bm),{bl_in} [np] "s"(np), [mk] "v"(mk) : RGF_CLOB);')
+            out.append(f'  asm volatile({fam}_SQROW_{a}("{bc}") : RGF_T_OPS(T) : RG_A_INS(A), RG_N_INS(N, "{nc}"), [bf] "v"(bf), [bm] "v"(bm),{bl_in} [np] "s"(np), [mk] "v"(mk) : RGF_CLOB);')
             out.append("}")
     out.append("template <int TPI> __device__ __forceinline__ void r27f_row(u64 (&T)[LL], const L27& A, u32 b, const Mod<TPI>& N, u32 np, u32 mk);")
-    for tpi, bc, fam in tpis:
+    for tpi, bc, fam, nc in tpis:
         out.append(f"template <> __device__ __forceinline__ void r27f_row<{tpi}>(u64 (&T)[LL], const L27& A, u32 b, const Mod<{tpi}>& N, u32 np, u32 mk) {{")
-        out.append(f'  asm volatile({fam}_ROW("{bc}") : RGF_T_OPS(T) : RG_A_INS(A), RG_N_INS(N, "v"), [b] "v"(b), [np] "s"(np), [mk] "v"(mk) : RGF_CLOB);')
+        out.append(f'  asm volatile({fam}_ROW("{bc}") : RGF_T_OPS(T) : RG_A_INS(A), RG_N_INS(N, "{nc}"), [b] "v"(b), [np] "s"(np), [mk] "v"(mk) : RGF_CLOB);')
         out.append("}")
     out.append("#elif RG_SECTION == 4")
     names = {n.split("(")[0] for n, _ in macros} | {n.split("(")[0] for lst in spread_macros.values() for n, _ in lst}

@@ -1,7 +1,7 @@
 # Same-box A/B of library variants: tools/gpu_job_ab.sh TAG [--no-tests] VARIANT...
 # (fate_amd/lib/ab/lib_<V>.so; "main" = fate_amd/lib/libfatephe.so).  Each variant: the parity
 # tests (unless --no-tests: a variant from before an ABI change), then two alternating
-# encrypt-only bench runs.
+# encrypt-only bench runs (or, with LEG=script.py, runs of tools/bench_legs/script.py).
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R
@@ -17,6 +17,11 @@ if [ $TESTS = 1 ]; then
 fi
 for rep in 1 2; do
   for V in "$@"; do
+    if [ -n "$LEG" ]; then  # LEG=script.py: a tools/bench_legs script printing one JSON line
+      FPHE_LIB_PATH=$(lib_of $V) timeout -k 10 300 python tools/bench_legs/$LEG > gpurun_out/${T}_${V}_b$rep.txt 2>&1 || { echo leg_failed $V; tail -30 gpurun_out/${T}_${V}_b$rep.txt; exit 1; }
+      echo "$V $(tail -1 gpurun_out/${T}_${V}_b$rep.txt)"
+      continue
+    fi
     FPHE_LIB_PATH=$(lib_of $V) timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-extras > gpurun_out/${T}_${V}_b$rep.txt 2>&1 || { echo bench_failed $V; tail -30 gpurun_out/${T}_${V}_b$rep.txt; exit 1; }
     python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['value'], d['roofline']['frac'], d['roofline']['kernel_ms'])" gpurun_out/${T}_${V}_b$rep.txt $V
   done
