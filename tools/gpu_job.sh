@@ -44,7 +44,7 @@ run_bench() {
 }
 run_prof() {
   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/${T}_trace -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline "$@" > $R/gpurun_out/${T}_trace_bench.txt 2>&1) || { echo trace_failed; tail -20 gpurun_out/${T}_trace_bench.txt; exit 1; }
-  tail -1 gpurun_out/${T}_trace_bench.txt > gpurun_out/${T}_trace_bench.json
+  grep '^{"metric"' gpurun_out/${T}_trace_bench.txt | tail -1 > gpurun_out/${T}_trace_bench.json
   echo prof_ok
 }
 pmc_pass() {  # pmc_pass NAME COUNTER CMD...
