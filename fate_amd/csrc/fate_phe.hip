@@ -791,6 +791,9 @@ struct CallBufs {
 };
 
 constexpr size_t kMaxFoldKeys = (size_t)1 << 25;  // (segment, exponent) buckets per call
+// one squaring on a lone wave (~35 us) in products of chip-wide fold throughput
+// (~1.6 ns each): the merge chain's price in k_gr_gapchoose
+constexpr long long kLoneSquaringProducts = 20000;
 
 fphe_status ensure_side(fphe_ctx* c) {
   if (c->side) return FPHE_OK;
@@ -1031,8 +1034,9 @@ fphe_status launch_fold_segments(fphe_ctx* c, const u32* Src, const u8* ssign, c
   size_t r = (T + round - 1) / round;
   r = r < 8 ? 8 : (r > (size_t)kSegFoldMax ? (size_t)kSegFoldMax : r);
   size_t nslots = (T + r - 1) / r;
-  // raised keys (group_dev.h k_gr_gapsel / k_gr_plan): keys >= 8 exponents above their
-  // segment's least one get slots of their own whose partials k_segfold27 raises in place.
+  // raised keys (group_dev.h k_gr_gapsel / k_gr_gapchoose / k_gr_plan): keys far enough above
+  // their segment's least exponent that raising them inside the balanced level costs less than
+  // their merge chain get slots of their own whose partials k_segfold27 raises in place.
   // FPHE_FOLD_RAISE=0 turns it off, =force raises every key above the least (tests).
   const char* rmode = getenv("FPHE_FOLD_RAISE");
   const bool rforce = rmode && !strcmp(rmode, "force");
@@ -1042,20 +1046,39 @@ fphe_status launch_fold_segments(fphe_ctx* c, const u32* Src, const u8* ssign, c
   if (raise) {
     const size_t smax = 2 * std::max(round, nslots) + 2 * (size_t)kRaiseMax + 2;
     if (smax < ((size_t)1 << 31)) {
-      int32_t* ng = B.get<int32_t>(1);
+      int32_t* ng = B.get<int32_t>(2);  // [0] keys recorded, [1] the chosen threshold
       int32_t* gk = B.get<int32_t>(5 * (size_t)kRaiseMax);
+      unsigned long long* ghist = B.get<unsigned long long>(kGapHist);
+      int32_t* gnum = B.get<int32_t>(kGapHist);
       plan = B.get<int32_t>(kPlanWords);
       raised = B.get<u8>(nkeys);
       if (!B.ok) return FPHE_ERR_HIP;
-      if (hipMemsetAsync(ng, 0, 4, s) != hipSuccess || hipMemsetAsync(raised, 0, nkeys, s) != hipSuccess)
+      if (hipMemsetAsync(ng, 0, 8, s) != hipSuccess || hipMemsetAsync(raised, 0, nkeys, s) != hipSuccess ||
+          hipMemsetAsync(ghist, 0, kGapHist * 8, s) != hipSuccess || hipMemsetAsync(gnum, 0, kGapHist * 4, s) != hipSuccess)
         return FPHE_ERR_HIP;
-      const int32_t gmin = rforce ? 1 : 8, xmax = rforce ? kI32Max : (int32_t)(r - 1);
-      hipLaunchKernelGGL(k_gr_gapsel, dim3(gr_grid(nseg, c->cus)), dim3(kGrBlock), 0, s, cntR, offR, nseg, (int32_t)NE,
-                         h[0], gmin, xmax, ng, gk, gk + kRaiseMax, gk + 2 * kRaiseMax, gk + 3 * kRaiseMax,
-                         gk + 4 * kRaiseMax);
+      const int32_t gmin = rforce ? 1 : 4, xmax = rforce ? kI32Max : (int32_t)(r - 1);
+      const unsigned gsg = gr_grid(nseg, c->cus);
+      int32_t* gsel = nullptr;
+      if (!rforce) {  // pass 1 and the threshold (group_dev.h); forced: every candidate
+        hipLaunchKernelGGL(k_gr_gapsel, dim3(gsg), dim3(kGrBlock), 0, s, cntR, offR, nseg, (int32_t)NE, h[0], gmin, xmax,
+                           (int32_t)r, ghist, gnum, (const int32_t*)nullptr, ng, gk, gk + kRaiseMax,
+                           gk + 2 * kRaiseMax, gk + 3 * kRaiseMax, gk + 4 * kRaiseMax);
+        gsel = ng + 1;
+        hipLaunchKernelGGL(k_gr_gapchoose, dim3(1), dim3(1), 0, s, ghist, gnum, gmin, kLoneSquaringProducts, gsel);
+      }
+      hipLaunchKernelGGL(k_gr_gapsel, dim3(gsg), dim3(kGrBlock), 0, s, cntR, offR, nseg, (int32_t)NE, h[0], gmin, xmax,
+                         (int32_t)r, (unsigned long long*)nullptr, (int32_t*)nullptr, (const int32_t*)gsel, ng, gk,
+                         gk + kRaiseMax, gk + 2 * kRaiseMax, gk + 3 * kRaiseMax, gk + 4 * kRaiseMax);
       hipLaunchKernelGGL(k_gr_plan, dim3(1), dim3(kGrBlock), 0, s, ng, gk, gk + kRaiseMax, gk + 2 * kRaiseMax,
                          gk + 3 * kRaiseMax, gk + 4 * kRaiseMax, (int64_t)T, (int32_t)round, (int32_t)r,
                          (int32_t)kSegFoldMax, (int32_t)smax, plan, raised);
+      if (getenv("FPHE_DEBUG")) {  // the plan's size (a read-back: debugging only)
+        int32_t ph[2] = {0, 0}, nh = 0;
+        if (hipMemcpyAsync(ph, plan, 8, hipMemcpyDeviceToHost, s) == hipSuccess &&
+            hipMemcpyAsync(&nh, ng, 4, hipMemcpyDeviceToHost, s) == hipSuccess && hipStreamSynchronize(s) == hipSuccess)
+          fprintf(stderr, "[fphe] fold plan: %d raise candidates, %d regions, %d slots (r0 %zu, round %zu, T %zu)\n", nh,
+                  ph[0], ph[1], r, round, T);
+      }
       nslots = smax;  // a bound: the plan's count is on the device (slots past it stay empty)
     }
   }

@@ -435,31 +435,85 @@ __global__ __launch_bounds__(kGrBlock) void k_gr_gaps(int32_t* __restrict__ exp,
 // A (segment, exponent) key far above its segment's least exponent -- the reference's rare
 // outliers, e.g. +-1e-30 or +-3.4e38 among gradients near 1 -- would need 4 gap squarings of its
 // partial in the exponent merge, on one wave after the whole fold.  Raised keys get slots of
-// their own in k_segfold27, which squares their partials there.  Per segment (one thread):
-// every key >= gmin exponents above the segment's least key exponent (jmin) is raised to it, if
-// raise_cost(gap) (its 4 gap squarings, in products) is at most xmax.  The least key may turn out to hold only
-// literal 1s; k_gr_gaps then reports it and the caller folds without the device merge.
+// their own in k_segfold27, which squares their partials there.  Candidates (one thread per
+// segment): keys >= gmin exponents above the segment's least key exponent (jmin) whose
+// raise_cost(gap) (4 gap squarings, in products) fits a slot (<= xmax).  Raising costs the
+// whole chip about (the key's slots) x raise_cost products; leaving a key to the merge costs its
+// chain, 4 gap squarings on one wave, but only the largest remaining gap counts.  So:
+//   pass 1 (hist != null): per gap, the candidates' summed raise cost and their number;
+//   k_gr_gapchoose: the least threshold G whose cost -- the raise costs of every candidate with
+//     gap >= G plus the chain of the largest gap left -- is lowest (no raising if that wins);
+//   pass 2 (gsel != null: records the keys with gap >= *gsel; null: every candidate).
+// The least key may turn out to hold only literal 1s; k_gr_gaps then reports it and the
+// caller folds without the device merge.
+constexpr int kGapHist = 512;  // gaps with raise_cost(gap) <= xmax < kSegFoldMax: < 256
 __global__ __launch_bounds__(kGrBlock) void k_gr_gapsel(const int32_t* __restrict__ cnt, const int32_t* __restrict__ off,
                                                         size_t nseg, int32_t NE, int32_t emin, int32_t gmin, int32_t xmax,
+                                                        int32_t r0, unsigned long long* __restrict__ hist,
+                                                        int32_t* __restrict__ hnum, const int32_t* __restrict__ gsel,
                                                         int32_t* __restrict__ ng, int32_t* __restrict__ gkey,
                                                         int32_t* __restrict__ gcnt, int32_t* __restrict__ goff,
                                                         int32_t* __restrict__ ggap, int32_t* __restrict__ gexp) {
+  const int32_t G = gsel ? *gsel : gmin;
+  if (G >= NE) return;  // k_gr_gapchoose chose no raising (or no gap can reach G)
   for (size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x; s < nseg; s += (size_t)gridDim.x * blockDim.x) {
     const int32_t* c = cnt + s * NE;
     int32_t jmin = 0;
     while (jmin < NE && c[jmin] == 0) ++jmin;
-    for (int32_t j = jmin + gmin; j < NE; ++j) {
-      if (c[j] == 0 || raise_cost(j - jmin) > xmax) continue;
+    for (int32_t j = jmin + (G > gmin ? G : gmin); j < NE; ++j) {
+      const int32_t g = j - jmin;
+      if (c[j] == 0 || raise_cost(g) > xmax) continue;
+      if (hist) {
+        const long long cap = r0 - raise_cost(g) > 1 ? r0 - raise_cost(g) : 1;
+        const int32_t gi = g < kGapHist ? g : kGapHist - 1;
+        atomicAdd(&hist[gi], (unsigned long long)(((long long)c[j] + cap - 1) / cap * raise_cost(g)));
+        atomicAdd(&hnum[gi], 1);
+        continue;
+      }
       const int32_t h = atomicAdd(ng, 1);
       if (h >= kRaiseMax) return;
       const int32_t k = (int32_t)(s * NE) + j;
       gkey[h] = k;
       gcnt[h] = c[j];
       goff[h] = off[k];
-      ggap[h] = j - jmin;
+      ggap[h] = g;
       gexp[h] = emin + jmin;
     }
   }
+}
+
+// One thread: the threshold of pass 2 (see above).  chain = the products of chip time one
+// squaring on a lone wave costs (~35 us against ~1.6 ns per product chip-wide); gaps below gmin
+// are never raised, so the chain left below the least threshold is bounded by gmin - 1.
+__global__ void k_gr_gapchoose(const unsigned long long* __restrict__ hist, const int32_t* __restrict__ hnum,
+                               int32_t gmin, long long chain, int32_t* __restrict__ gsel) {
+  int32_t gmax = 0;
+  for (int32_t g = kGapHist - 1; g >= gmin; --g)
+    if (hnum[g]) {
+      gmax = g;
+      break;
+    }
+  int32_t best_g = kI32Max;  // no raising
+  long long best = gmax ? 4ll * gmax * chain : 0;
+  long long w = 0;
+  int32_t n = 0;
+  for (int32_t G = gmax; G >= gmin && gmax; --G) {
+    w += (long long)hist[G];
+    n += hnum[G];
+    if (n > kRaiseMax) break;
+    int32_t rem = gmin - 1;  // the largest gap left to the merge
+    for (int32_t g = G - 1; g >= gmin; --g)
+      if (hnum[g]) {
+        rem = g;
+        break;
+      }
+    const long long cost = w + 4ll * rem * chain;
+    if (hnum[G] && cost < best) {
+      best = cost;
+      best_g = G;
+    }
+  }
+  *gsel = best_g;
 }
 
 // One workgroup: the slot plan (kernels27.h) for the raised keys k_gr_gapsel found.  Regions in

@@ -217,10 +217,9 @@ def test_fold_raised_keys_forced(env, monkeypatch):
 
 @pytest.mark.parametrize("bits", [2048])
 def test_fold_raised_keys_auto_matches_merge(bits, monkeypatch):
-    """The automatic raise (keys >= 8 exponents above their segment's least, at a size where
-    the balanced level has room for their squarings: 2.1M terms) returns the same integers as
-    the plain exponent merge (FPHE_FOLD_RAISE=0), with outliers 9 and 10 exponents above and
-    below the bulk of their segments."""
+    """The automatic choice at 2.1M terms, outliers 9 and 10 exponents above and below the
+    bulk of their segments (k_gr_gapchoose weighs raising each segment's bulk against the
+    merge's chain) returns the same integers as the plain exponent merge (FPHE_FOLD_RAISE=0)."""
     fx, sk, pk, coder, opk, cts = load(bits)
     base = more(opk, cts, 512, 31)
     rng = random.Random(31)
@@ -237,3 +236,49 @@ def test_fold_raised_keys_auto_matches_merge(bits, monkeypatch):
     monkeypatch.setenv("FPHE_FOLD_RAISE", "0")
     want = host(pk, P._fold_to_segments(pk, v, seg, 64, index=idx))
     assert got == want
+
+
+def test_fold_raised_keys_past_the_cap(env, monkeypatch):
+    """More keys to raise than the plan takes (kRaiseMax = 512): 600 segments each with a term
+    8 exponents above its least one.  The keys past the cap stay in the exponent merge; every
+    segment is still the reference's fold."""
+    fx, sk, pk, coder, opk, cts = env
+    base = more(opk, cts, 40, 41)
+    rng = random.Random(41)
+    nseg = 600
+    src, seg = [], []
+    for s_ in range(nseg):
+        for e in (-13, -5, -13):
+            src.append(O.Ciphertext(base[rng.randrange(len(base))].c, e))
+            seg.append(s_)
+    idx = list(range(len(src)))
+    want = oracle_fold(opk, src, idx, seg, nseg)
+    monkeypatch.setenv("FPHE_FOLD_RAISE", "force")
+    got = P._fold_to_segments(pk, dev_vec(pk, src), torch.tensor(seg), nseg)
+    assert host(pk, got) == want
+
+
+def test_fold_raised_keys_multi_round_plan(monkeypatch):
+    """A fold longer than one round of balanced slots at the largest slot length (36M terms
+    against 32,768 slots x 1,024 items at 2048 bits), with outlier keys 9-12 exponents away:
+    the plain merge, the automatic raise and the forced raise give the same integers."""
+    fx, sk, pk, coder, opk, cts = load(2048)
+    base = more(opk, cts, 256, 43)
+    exps = [-13] * 256
+    for i in range(0, 256, 29):
+        exps[i] = -13 + (9 if i % 2 else -12)
+    v = dev_vec(pk, [O.Ciphertext(c.c, e) for c, e in zip(base, exps)])
+    g = torch.Generator().manual_seed(43)
+    T = 36_000_000
+    idx = torch.randint(0, 256, (T,), generator=g, dtype=torch.int32).cuda()
+    seg = torch.randint(0, 500, (T,), generator=g, dtype=torch.int32).cuda()  # 500 x 22 keys: LDS counts
+    outs = []
+    for mode in ("0", None, "force"):
+        if mode is None:
+            monkeypatch.delenv("FPHE_FOLD_RAISE", raising=False)
+        else:
+            monkeypatch.setenv("FPHE_FOLD_RAISE", mode)
+        r = P._fold_to_segments(pk, v, seg, 500, index=idx)
+        outs.append((r.C[: (500 + 63) // 64].clone(), r.sign[:500].clone(), r.exp[:500].clone()))
+    for o in outs[1:]:
+        assert all(torch.equal(a, b) for a, b in zip(outs[0], o))
