@@ -487,6 +487,12 @@ __global__ __launch_bounds__(kGrBlock) void k_gr_gapsel(const int32_t* __restric
 // are never raised, so the chain left below the least threshold is bounded by gmin - 1.
 __global__ void k_gr_gapchoose(const unsigned long long* __restrict__ hist, const int32_t* __restrict__ hnum,
                                int32_t gmin, long long chain, int32_t* __restrict__ gsel) {
+  __shared__ int32_t below[kGapHist];  // below[G]: the largest candidate gap < G (gmin - 1: none)
+  int32_t last = gmin - 1;
+  for (int32_t g = 0; g < kGapHist; ++g) {
+    below[g] = last;
+    if (g >= gmin && hnum[g]) last = g;
+  }
   int32_t gmax = 0;
   for (int32_t g = kGapHist - 1; g >= gmin; --g)
     if (hnum[g]) {
@@ -501,12 +507,7 @@ __global__ void k_gr_gapchoose(const unsigned long long* __restrict__ hist, cons
     w += (long long)hist[G];
     n += hnum[G];
     if (n > kRaiseMax) break;
-    int32_t rem = gmin - 1;  // the largest gap left to the merge
-    for (int32_t g = G - 1; g >= gmin; --g)
-      if (hnum[g]) {
-        rem = g;
-        break;
-      }
+    const int32_t rem = below[G];  // the largest gap left to the merge
     const long long cost = w + 4ll * rem * chain;
     if (hnum[G] && cost < best) {
       best = cost;
