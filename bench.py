@@ -102,9 +102,15 @@ def enc_mad27_per_elem(key_bits: int, n: int) -> float:
 
 
 def enc_crt_mac32_per_elem(key_bits: int) -> float:
-    # key-holder encrypt: two E-bit-exponent modexps over the L/2-limb p^2, q^2 (E = bits of
-    # n mod s(s-1), ~key_bits), w=5 fixed-window formula of SURVEY.md §8(d), + 4 products
-    # of the recombination over n^2
+    # key-holder encrypt, the w=5 fixed-window formula of SURVEY.md §8(d) for the modexps it
+    # runs, + 4 products of the recombination over n^2.  Keys above 1024 bits (the split,
+    # FPHE_KH_SPLIT): per half z = r^(q mod (p-1)) mod p over the key/64-limb p,
+    # then z^p mod p^2 over the key/32-limb p^2, both with (key/2)-bit exponents; up to 1024
+    # bits: one (n mod s(s-1))-bit (~key_bits) exponent mod s^2 per half
+    if key_bits > 1024:
+        E = key_bits // 2
+        per_half = (E + math.ceil(E / 5) + 16) * (mac32_per_mont(key_bits // 64) + mac32_per_mont(key_bits // 32))
+        return 2 * per_half + 4 * mac32_per_mont(key_bits // 16)
     E = key_bits
     return 2 * (E + math.ceil(E / 5) + 16) * mac32_per_mont(key_bits // 32) + 4 * mac32_per_mont(key_bits // 16)
 

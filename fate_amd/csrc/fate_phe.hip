@@ -70,6 +70,14 @@ struct KeyArgs {
   const u32* N2R3_27;                    // R^3 mod n^2                                  [NL2]
   const u32* P2RX_27; const u32* Q2RX_27;  // R_s^2 R^-1 mod s^2, s = p, q                [NLh]
   const u32* N2M1;                       // M(1) = R mod n^2 in 32-bit words (literal 1)  [L2]
+  // key-holder encryption in two steps (FPHE_KH_SPLIT): z_s = r^(e_s)
+  // mod s with e_p = q mod (p-1), e_q = p mod (q-1), on the engine of s (TPIs = L2/128 lanes,
+  // at least 1), then x_s = z_s^s mod s^2 on the s^2 engine
+  const u32* Ps_27; const u32* PsR2_27; const u32* PsR3_27;  // p, R_s^2, R_s^3 mod p      [NLs]
+  const u32* Qs_27; const u32* QsR2_27; const u32* QsR3_27;
+  u32 ps_np27, qs_np27;
+  const u32* e1p; const u32* e1q;        // q mod (p-1), p mod (q-1)                   [LQ]
+  int e1p_bits, e1q_bits, p_bits, q_bits;
 };
 
 __device__ __forceinline__ void set_err(int32_t* err, u32 f) {
@@ -701,17 +709,31 @@ fphe_status launch_encrypt_crt27(fphe_ctx* c, const uint32_t* P, uint32_t lp, co
                                  uint8_t* sign, hipStream_t s) {
   constexpr int TPIh = L / 64, Eh = FPHE_WAVE / TPIh, NLh = rad_ll(TPIh) * TPIh, L1 = L / 2;
   constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = rad_ll(TPI) * TPI, LDSW = NL > L + 3 ? NL : L + 3;
+  constexpr int TPIs = L >= 128 ? L / 128 : 1, Es = FPHE_WAVE / TPIs, NLs = rad_ll(TPIs) * TPIs;
   auto k1 = KS<TPIh>::template pow_half<L, kWinSlide, true>();
   const size_t lds1 = (size_t)kWavesPerBlock * NLh * Eh * 4;
   set_lds(k1, lds1);
   const size_t span = span_elems(c, k1, lds1, Eh);
   const size_t m0 = count < span ? count : span;
   const unsigned g1 = occ_grid(c, k1, lds1, (m0 + Eh - 1) / Eh, "pow_half27<enc>");
-  const size_t tbytes = (size_t)g1 * kWavesPerBlock * kTabEntries<kWinSlide> * rad_ll(TPIh) * FPHE_WAVE * 4;
+  size_t tbytes = (size_t)g1 * kWavesPerBlock * kTabEntries<kWinSlide> * rad_ll(TPIh) * FPHE_WAVE * 4;
+  // the split modexp's first step (FPHE_KH_SPLIT): z_s = r^(e_s) mod s into Z, then k1 raises
+  // z_s to s mod s^2; both share the window-table region
+  auto k0 = KS<TPIs>::template pow_small<L, kWinSlide>();
+  const size_t lds0 = (size_t)kWavesPerBlock * NLs * Es * 4;
+  unsigned g0 = 0;
+  size_t zbytes = 0;
+  if (kKhSplit<L>) {
+    set_lds(k0, lds0);
+    g0 = occ_grid(c, k0, lds0, (m0 + Es - 1) / Es, "pow_small27");
+    tbytes = std::max(tbytes, (size_t)g0 * kWavesPerBlock * kTabEntries<kWinSlide> * rad_ll(TPIs) * FPHE_WAVE * 4);
+    zbytes = (size_t)ntiles_of(m0) * 2 * kZWords<L> * FPHE_WAVE * 4;
+  }
   const size_t ybytes = (size_t)ntiles_of(m0) * 2 * L1 * FPHE_WAVE * 4;
   const size_t rbytes = (size_t)ntiles_of(m0) * L1 * FPHE_WAVE * 4;
-  if (ensure_scratch(c, tbytes + ybytes + (r ? 0 : rbytes), s) != FPHE_OK) return FPHE_ERR_HIP;
+  if (ensure_scratch(c, tbytes + ybytes + zbytes + (r ? 0 : rbytes), s) != FPHE_OK) return FPHE_ERR_HIP;
   u32* Y = c->scratch + tbytes / 4;
+  u32* Z = Y + ybytes / 4;
   ChaChaKey ck;
   if (!r)
     for (int i = 0; i < 8; ++i) ck.k[i] = key[i];
@@ -723,12 +745,17 @@ fphe_status launch_encrypt_crt27(fphe_ctx* c, const uint32_t* P, uint32_t lp, co
     const size_t m = count - e0 < span ? count - e0 : span, t0 = e0 / FPHE_WAVE;
     const u32* rbuf = r ? r + t0 * L1 * FPHE_WAVE : nullptr;
     if (!r) {
-      u32* rdev = Y + ybytes / 4;
+      u32* rdev = Z + zbytes / 4;
       const unsigned rgrid = (unsigned)std::min<size_t>((m + 255) / 256, (size_t)c->cus * 4);
       hipLaunchKernelGGL(k_draw_r<L1>, dim3(rgrid), dim3(256), 0, s, c->K, m, ck, nonce, e0, rdev);
       rbuf = rdev;
     }
-    hipLaunchKernelGGL(k1, dim3(g1), dim3(kBlock), lds1, s, c->K, rbuf, m, Y, c->scratch, (u32)NLh);
+    if (kKhSplit<L>) {
+      hipLaunchKernelGGL(k0, dim3(g0), dim3(kBlock), lds0, s, c->K, rbuf, m, Z, c->scratch, (u32)NLs);
+      hipLaunchKernelGGL(k1, dim3(g1), dim3(kBlock), lds1, s, c->K, (const u32*)Z, m, Y, c->scratch, (u32)NLh);
+    } else {
+      hipLaunchKernelGGL(k1, dim3(g1), dim3(kBlock), lds1, s, c->K, rbuf, m, Y, c->scratch, (u32)NLh);
+    }
     hipLaunchKernelGGL(k2, dim3(g2), dim3(kBlock), lds2, s, c->K, P + t0 * lp * FPHE_WAVE, lp, neg + e0, m, Y,
                        C + t0 * L * FPHE_WAVE, sign + e0, (u32)LDSW);
     if (hipGetLastError() != hipSuccess) return FPHE_ERR_HIP;
@@ -1630,6 +1657,9 @@ fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, 
     u32 p2n0 = 0, pn0 = 0, q2n0 = 0, qn0 = 0;
     int pm1b = 0, qm1b = 0, epb = 0, eqb = 0;
     size_t o_ep = 0, o_eq = 0, o_KpR = 0, o_KqR = 0, o_P2RX_27 = 0, o_Q2RX_27 = 0;
+    size_t o_Ps = 0, o_PsR2 = 0, o_PsR3 = 0, o_Qs = 0, o_QsR2 = 0, o_QsR3 = 0, o_e1p = 0, o_e1q = 0;
+    u32 ps_np = 0, qs_np = 0;
+    int e1pb = 0, e1qb = 0, pb = 0, qb = 0;
     const bool has_sk = p_w != nullptr;
     if (has_sk) {
       Limbs p = from_words(p_w, LQ), q = from_words(q_w, LQ);
@@ -1681,6 +1711,22 @@ fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, 
       o_ep = put(ep, L1);
       o_eq = put(eq, L1);
       epb = (int)hbn::bitlen(ep); eqb = (int)hbn::bitlen(eq);
+      {  // the split key-holder modexp's constants (KeyArgs)
+        const int TPIs = L2 >= 128 ? L2 / 128 : 1, LBs = rad_lb(TPIs), NLs = rad_ll(TPIs) * TPIs;
+        o_Ps = put(to27(p, NLs, LBs), NLs);
+        o_PsR2 = put(to27(hbn::pow2_mod((size_t)2 * LBs * NLs, p), NLs, LBs), NLs);
+        o_PsR3 = put(to27(hbn::pow2_mod((size_t)3 * LBs * NLs, p), NLs, LBs), NLs);
+        o_Qs = put(to27(q, NLs, LBs), NLs);
+        o_QsR2 = put(to27(hbn::pow2_mod((size_t)2 * LBs * NLs, q), NLs, LBs), NLs);
+        o_QsR3 = put(to27(hbn::pow2_mod((size_t)3 * LBs * NLs, q), NLs, LBs), NLs);
+        ps_np = hbn::neg_inv32(p[0]) & ((1u << LBs) - 1u);
+        qs_np = hbn::neg_inv32(q[0]) & ((1u << LBs) - 1u);
+        const Limbs e1p = hbn::mod(q, pm1), e1q = hbn::mod(p, qm1);
+        o_e1p = put(e1p, LQ);
+        o_e1q = put(e1q, LQ);
+        e1pb = (int)hbn::bitlen(e1p); e1qb = (int)hbn::bitlen(e1q);
+        pb = (int)hbn::bitlen(p); qb = (int)hbn::bitlen(q);
+      }
       const Limbs R27 = hbn::pow2_mod((size_t)LB2 * NL2, N2);
       const Limbs Kp = hbn::mul(Q2, hbn::inv_mod(hbn::mod(Q2, P2), P2));  // < n^2
       const Limbs Kq = hbn::mul(P2, hbn::inv_mod(hbn::mod(P2, Q2), Q2));
@@ -1733,6 +1779,11 @@ fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, 
       K.ep = b + o_ep; K.eq = b + o_eq; K.ep_bits = epb; K.eq_bits = eqb;
       K.KpR_27 = b + o_KpR; K.KqR_27 = b + o_KqR;
       K.P2RX_27 = b + o_P2RX_27; K.Q2RX_27 = b + o_Q2RX_27;
+      K.Ps_27 = b + o_Ps; K.PsR2_27 = b + o_PsR2; K.PsR3_27 = b + o_PsR3;
+      K.Qs_27 = b + o_Qs; K.QsR2_27 = b + o_QsR2; K.QsR3_27 = b + o_QsR3;
+      K.ps_np27 = ps_np; K.qs_np27 = qs_np;
+      K.e1p = b + o_e1p; K.e1q = b + o_e1q;
+      K.e1p_bits = e1pb; K.e1q_bits = e1qb; K.p_bits = pb; K.q_bits = qb;
     }
     *out = c;
     return FPHE_OK;

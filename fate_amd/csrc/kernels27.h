@@ -104,6 +104,19 @@ __device__ __forceinline__ ColIO colio(const u32* tile_base, u32 rows, u32 col, 
   return c;
 }
 
+// key-holder encrypt in two modexp steps (k_pow_small27, then k_pow_half27<., ., true>);
+// 0: one |n|-bit exponent mod s^2 per half (A/B)
+#ifndef FPHE_KH_SPLIT
+#define FPHE_KH_SPLIT 1
+#endif
+// words per half of the step-1 values z_s (< s): one lane's 32-word chunk per lane of s's
+// engine (TPIs = L/128 lanes, at least 1)
+template <int L>
+constexpr uint32_t kZWords = 32u * (L >= 128 ? L / 128 : 1);
+// the split pays where s runs on a smaller engine than s^2 (keys > 1024 bits); at 1024 bits
+// both are 37-limb TPI-1 engines and the split only adds work (same-box -1.5%)
+template <int L>
+constexpr bool kKhSplit = FPHE_KH_SPLIT && L >= 128;
 constexpr int kFoldMax = 64;  // terms per k_fold27 chunk
 // items per wave slot of the balanced first fold level (k_segfold27), at most
 constexpr int kSegFoldMax = 1024;
