@@ -1087,15 +1087,17 @@ fphe_status launch_fold_segments(fphe_ctx* c, const u32* Src, const u8* ssign, c
       const unsigned gsg = gr_grid(nseg, c->cus);
       int32_t* gsel = nullptr;
       if (!rforce) {  // pass 1 and the threshold (group_dev.h); forced: every candidate
-        hipLaunchKernelGGL(k_gr_gapsel, dim3(gsg), dim3(kGrBlock), 0, s, cntR, offR, nseg, (int32_t)NE, h[0], gmin, xmax,
-                           (int32_t)r, ghist, gnum, (const int32_t*)nullptr, ng, gk, gk + kRaiseMax,
-                           gk + 2 * kRaiseMax, gk + 3 * kRaiseMax, gk + 4 * kRaiseMax);
+        hipLaunchKernelGGL(k_gr_gapsel<L>, dim3(gsg), dim3(kGrBlock), 0, s, cntR, offR, nseg, (int32_t)NE, h[0], gmin,
+                           xmax, (int32_t)r, (const int32_t*)ord, Src, ssign, c->K.N2M1, ghist, gnum,
+                           (const int32_t*)nullptr, ng, gk, gk + kRaiseMax, gk + 2 * kRaiseMax, gk + 3 * kRaiseMax,
+                           gk + 4 * kRaiseMax);
         gsel = ng + 1;
         hipLaunchKernelGGL(k_gr_gapchoose, dim3(1), dim3(1), 0, s, ghist, gnum, gmin, kLoneSquaringProducts, gsel);
       }
-      hipLaunchKernelGGL(k_gr_gapsel, dim3(gsg), dim3(kGrBlock), 0, s, cntR, offR, nseg, (int32_t)NE, h[0], gmin, xmax,
-                         (int32_t)r, (unsigned long long*)nullptr, (int32_t*)nullptr, (const int32_t*)gsel, ng, gk,
-                         gk + kRaiseMax, gk + 2 * kRaiseMax, gk + 3 * kRaiseMax, gk + 4 * kRaiseMax);
+      hipLaunchKernelGGL(k_gr_gapsel<L>, dim3(gsg), dim3(kGrBlock), 0, s, cntR, offR, nseg, (int32_t)NE, h[0], gmin,
+                         xmax, (int32_t)r, (const int32_t*)ord, Src, ssign, c->K.N2M1, (unsigned long long*)nullptr,
+                         (int32_t*)nullptr, (const int32_t*)gsel, ng, gk, gk + kRaiseMax, gk + 2 * kRaiseMax,
+                         gk + 3 * kRaiseMax, gk + 4 * kRaiseMax);
       hipLaunchKernelGGL(k_gr_plan, dim3(1), dim3(kGrBlock), 0, s, ng, gk, gk + kRaiseMax, gk + 2 * kRaiseMax,
                          gk + 3 * kRaiseMax, gk + 4 * kRaiseMax, (int64_t)T, (int32_t)round, (int32_t)r,
                          (int32_t)kSegFoldMax, (int32_t)smax, plan, raised);

@@ -447,9 +447,41 @@ __global__ __launch_bounds__(kGrBlock) void k_gr_gaps(int32_t* __restrict__ exp,
 // The least key may turn out to hold only literal 1s; k_gr_gaps then reports it and the
 // caller folds without the device merge.
 constexpr int kGapHist = 512;  // gaps with raise_cost(gap) <= xmax < kSegFoldMax: < 256
+// Is source element i the literal 1 (M(1) words, sign 0)?  Tile-major words, 256 B apart.
+template <int L>
+__device__ __forceinline__ bool gr_is_literal(const u32* __restrict__ Src, const u8* __restrict__ ssign,
+                                              const u32* __restrict__ one, int32_t i) {
+  if (ssign[i]) return false;
+  const u32* c = Src + ((size_t)(i >> 6) * L) * FPHE_WAVE + (i & 63);
+  for (int j = 0; j < L; ++j)
+    if (c[(size_t)j * FPHE_WAVE] != one[j]) return false;
+  return true;
+}
+
+// The segment's least exponent among keys holding a non-literal term -- the e_min the
+// reference aligns to (literal 1s are add's identity): usually the least key's first term
+// settles it.  NE when the segment holds only literal 1s.
+template <int L>
+__device__ __forceinline__ int32_t gr_seg_jmin(const int32_t* __restrict__ c, const int32_t* __restrict__ off,
+                                               size_t s, int32_t NE, const int32_t* __restrict__ ord,
+                                               const u32* __restrict__ Src, const u8* __restrict__ ssign,
+                                               const u32* __restrict__ one) {
+  for (int32_t j = 0; j < NE; ++j) {
+    if (c[j] == 0) continue;
+    const int32_t o = off[s * NE + j];
+    for (int32_t t = 0; t < c[j]; ++t)
+      if (!gr_is_literal<L>(Src, ssign, one, ord[o + t])) return j;
+  }
+  return NE;
+}
+
+template <int L>
 __global__ __launch_bounds__(kGrBlock) void k_gr_gapsel(const int32_t* __restrict__ cnt, const int32_t* __restrict__ off,
                                                         size_t nseg, int32_t NE, int32_t emin, int32_t gmin, int32_t xmax,
-                                                        int32_t r0, unsigned long long* __restrict__ hist,
+                                                        int32_t r0, const int32_t* __restrict__ ord,
+                                                        const u32* __restrict__ Src, const u8* __restrict__ ssign,
+                                                        const u32* __restrict__ one,
+                                                        unsigned long long* __restrict__ hist,
                                                         int32_t* __restrict__ hnum, const int32_t* __restrict__ gsel,
                                                         int32_t* __restrict__ ng, int32_t* __restrict__ gkey,
                                                         int32_t* __restrict__ gcnt, int32_t* __restrict__ goff,
@@ -458,8 +490,10 @@ __global__ __launch_bounds__(kGrBlock) void k_gr_gapsel(const int32_t* __restric
   if (G >= NE) return;  // k_gr_gapchoose chose no raising (or no gap can reach G)
   for (size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x; s < nseg; s += (size_t)gridDim.x * blockDim.x) {
     const int32_t* c = cnt + s * NE;
-    int32_t jmin = 0;
-    while (jmin < NE && c[jmin] == 0) ++jmin;
+    int32_t jfirst = 0;
+    while (jfirst < NE && c[jfirst] == 0) ++jfirst;
+    if (jfirst + (G > gmin ? G : gmin) >= NE) continue;  // no key far enough up: nothing to check
+    const int32_t jmin = gr_seg_jmin<L>(c, off, s, NE, ord, Src, ssign, one);
     for (int32_t j = jmin + (G > gmin ? G : gmin); j < NE; ++j) {
       const int32_t g = j - jmin;
       if (c[j] == 0 || raise_cost(g) > xmax) continue;
