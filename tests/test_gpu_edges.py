@@ -530,7 +530,7 @@ def test_config2_subset_4096_vs_gmp():
 
 
 @pytest.mark.parametrize("bits", [3072])
-def test_large_key_vector_ops_and_pickle(bits):
+def test_large_key_vector_ops_and_pickle(bits, monkeypatch):
     """The 4096-bit geometry (TPI 8) through the vector ops above the element-wise kernels:
     the device-grouped fold under iupdate (terms with several exponents, negative signed
     ciphertexts, literal 1s), cumsum, and the reference's pickle state (bincode of the signed
@@ -560,6 +560,13 @@ def test_large_key_vector_ops_and_pickle(bits):
     want = [O.ct_zero() for _ in range(nslot * 2)]
     O.iupdate(opk, want, src, positions, 2)
     assert hist.to_signed_ints(pk.ns) == ([c.c for c in want], [c.exp for c in want])
+    # the same fold with every key above its slot's least exponent raised inside k_segfold27
+    # (the slot plan on the TPI-8 geometry)
+    monkeypatch.setenv("FPHE_FOLD_RAISE", "force")
+    hist2 = P.CiphertextVector.zeros(nslot * 2, pk._key.L2)
+    hist2.iupdate(dv, positions, 2, pk)
+    monkeypatch.delenv("FPHE_FOLD_RAISE")
+    assert hist2.to_signed_ints(pk.ns) == ([c.c for c in want], [c.exp for c in want])
     # cumsum with step 1 over two chunks
     cv = P.CiphertextVector.from_signed_ints([c.c for c in src[:40]], [c.exp for c in src[:40]], pk.ns, pk._key.L2)
     cv.chunking_cumsum_with_step(pk, [25, 15], 1)
