@@ -9,7 +9,8 @@
 #       pmc       FETCH_SIZE / WRITE_SIZE passes (one counter per run): the encrypt kernel over
 #                 bench.py --n 131072, the op kernels over tools/bench_legs/ops_pmc_leg.py,
 #                 summarised into gpurun_out/TAG_pmc_encrypt27.json / TAG_pmc_ops.json
-#       sq        SQ / GRBM counter passes over tools/bench_legs/ops_pmc_leg.py
+#       sq        SQ / GRBM counter passes over tools/bench_legs/ops_pmc_leg.py (or the leg
+#                 script named by args, e.g. k1024_leg.py), tabled into gpurun_out/TAG_sq.txt
 #       evidence  round, then prof, then pmc (the end-of-round record for profiles/)
 #       leg       python tools/bench_legs/ARGS (one bench leg script)
 #       timeline  rocprofv3 kernel trace of tools/bench_legs/hist_leg.py ARGS (PHASES=0), last
@@ -62,8 +63,11 @@ run_pmc() {
   grep hbm_bytes_per_elem gpurun_out/${T}_pmc_encrypt27.json
 }
 run_sq() {
-  pmc_pass sq "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE GRBM_COUNT" python3 $R/tools/bench_legs/ops_pmc_leg.py
-  pmc_pass sq2 "SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_LDS_BANK_CONFLICT SQ_INSTS_BRANCH" python3 $R/tools/bench_legs/ops_pmc_leg.py
+  local leg=${1:-ops_pmc_leg.py}
+  [ $# -gt 0 ] && shift
+  pmc_pass sq "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE GRBM_COUNT" python3 $R/tools/bench_legs/$leg "$@"
+  pmc_pass sq2 "SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_LDS_BANK_CONFLICT SQ_INSTS_BRANCH" python3 $R/tools/bench_legs/$leg "$@"
+  python tools/pmc_sq_compare.py gpurun_out/${T}_sq gpurun_out/${T}_sq2 > gpurun_out/${T}_sq.txt || exit 1
   echo sq_ok
 }
 
@@ -73,7 +77,7 @@ case $M in
   bench) run_bench "$@" ;;
   prof) run_prof "$@" ;;
   pmc) run_pmc ;;
-  sq) run_sq ;;
+  sq) run_sq "$@" ;;
   sqhist)  # SQ / GRBM counters over tools/bench_legs/hist_leg.py ARGS (PHASES=0)
     export PHASES=0
     pmc_pass sqh "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE GRBM_COUNT" python3 $R/tools/bench_legs/hist_leg.py "$@"
