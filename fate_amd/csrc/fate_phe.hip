@@ -26,6 +26,14 @@ namespace {
 constexpr int kBlock = 256;      // 4 waves per workgroup
 constexpr int kWavesPerBlock = kBlock / FPHE_WAVE;
 constexpr int kWinSlide = 6;     // sliding window of the 27-bit engine's shared-exponent modexps
+// the decrypt halves of <= 1024-bit keys (TPI 1, exponents p-1 / q-1 of <= 512 bits): a 5-bit
+// window builds 16 fewer table entries than it adds window products (~101 general products
+// against ~105 at 6 bits), and halves the per-lane table
+#ifndef FPHE_WIN_DEC1
+#define FPHE_WIN_DEC1 5
+#endif
+template <int TPI>
+constexpr int kWinDec = TPI == 1 ? FPHE_WIN_DEC1 : kWinSlide;
 constexpr int kWinMul = 4;       // window of the per-lane-exponent modexp (ct x pt): table capacity
 #ifndef FPHE_MUL_ADAPT
 #define FPHE_MUL_ADAPT 1  // ct x pt: 3-bit window for short exponents, all-zero windows skipped
@@ -677,13 +685,13 @@ fphe_status launch_encrypt27(fphe_ctx* c, const uint32_t* P, uint32_t lp, const 
 template <int L>
 fphe_status launch_decrypt27(fphe_ctx* c, const uint32_t* C, size_t count, uint32_t* P, hipStream_t s) {
   constexpr int TPI = L / 64, E = FPHE_WAVE / TPI, NL = rad_ll(TPI) * TPI, LH = L / 2, LQ = L / 4;
-  auto kern = KS<TPI>::template pow_half<L, kWinSlide, false>();
+  auto kern = KS<TPI>::template pow_half<L, kWinDec<TPI>, false>();
   const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
   set_lds(kern, lds);
   const size_t span = span_elems(c, kern, lds, E);
   const size_t m0 = count < span ? count : span;
   const unsigned grid = occ_grid(c, kern, lds, (m0 + E - 1) / E, "decrypt_pow27");
-  const size_t tbytes = (size_t)grid * kWavesPerBlock * kTabEntries<kWinSlide> * rad_ll(TPI) * FPHE_WAVE * 4;
+  const size_t tbytes = (size_t)grid * kWavesPerBlock * kTabEntries<kWinDec<TPI>> * rad_ll(TPI) * FPHE_WAVE * 4;
   const size_t ybytes = (size_t)ntiles_of(m0) * 2 * LH * FPHE_WAVE * 4;
   if (ensure_scratch(c, tbytes + ybytes, s) != FPHE_OK) return FPHE_ERR_HIP;
   u32* Y = c->scratch + tbytes / 4;

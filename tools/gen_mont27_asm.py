@@ -53,6 +53,36 @@ def gen(LL, LB):
     for a in range(LL):
         body = "".join(f'"v_mad_u64_u32 %[t{k}], vcc, %[a{k}], %[{mul}], %[t{k}]\\n\\t" ' for k, mul in window(a))
         macros.append((f"RG_SQROW_{a}", body))
+    # TPI-1 rows with the top accumulator limb kept logically zero instead of zeroed after every
+    # reduction row (FPHE_TPI1_TOPZ, mont_engine.inc): the operand row writing t_{LL-1} first
+    # adds to the constant 0 (its operand is output-only), and a reduction row after an operand
+    # row that left t_{LL-1} alone reads 0 in its place
+    top = LL - 1
+    macros.append(("RG_OPROW_Z", "".join(
+        f'"v_mad_u64_u32 %[t{j}], vcc, %[a{j}], %[b], {"0" if j == top else f"%[t{j}]"}\\n\\t" ' for j in range(LL))))
+    macros.append(("RG_REDROW_Z", red.replace(f"%[t{top}]\\n", "0\\n")))
+    for a in range(LL):
+        if any(k == top for k, _ in window(a)):
+            body = "".join(f'"v_mad_u64_u32 %[t{k}], vcc, %[a{k}], %[{mul}], {"0" if k == top else f"%[t{k}]"}\\n\\t" '
+                           for k, mul in window(a))
+            macros.append((f"RG_SQROZ_{a}", body))
+    # ... and a product's first rows over an accumulator that is still all zero, so no
+    # 64-bit zero stores start the product: RG_OPROW_F writes every limb over 0, RG_SQROW_F0
+    # squaring row 0's window over 0, RG_REDROW_F0 the reduction row after it (reads 0 for the
+    # limbs outside that window)
+    live0 = sorted(k for k, _ in window(0))
+    macros.append(("RG_OPROW_F", "".join(f'"v_mad_u64_u32 %[t{j}], vcc, %[a{j}], %[b], 0\\n\\t" ' for j in range(LL))))
+    macros.append(("RG_SQROW_F0", "".join(f'"v_mad_u64_u32 %[t{k}], vcc, %[a{k}], %[{mul}], 0\\n\\t" ' for k, mul in window(0))))
+    redf = '"v_mad_u64_u32 %[x], vcc, %[m], %[n0], %[t0]\\n\\t" '
+    redf += "".join(f'"v_mad_u64_u32 %[t{j-1}], vcc, %[m], %[n{j}], {f"%[t{j}]" if j in live0 else "0"}\\n\\t" '
+                    for j in range(1, LL))
+    macros.append(("RG_REDROW_F0", redf))
+    macros.append(("RG_T_OUT_ALL(T)", ", ".join(f'[t{j}] "=&v"(T[{j}])' for j in range(LL))))
+    macros.append(("RG_T_SQ0_OUT(T)", ", ".join(f'[t{k}] "=&v"(T[{k}])' for k in live0)))
+    macros.append(("RG_T_F0_OPS(T)", ", ".join(
+        f'[t{j}] "+v"(T[{j}])' if j in live0 else f'[t{j}] "=&v"(T[{j}])' for j in range(LL - 1))))
+    macros.append(("RG_T_TOP_OUT(T)", f'[t{top}] "=&v"(T[{top}])'))
+    macros.append(("RG_T_OPS_LO(T)", ", ".join(f'[t{j}] "+v"(T[{j}])' for j in range(LL - 1))))
     macros.append(("RG_T_OPS(T)", ", ".join(f'[t{j}] "+v"(T[{j}])' for j in range(LL))))
     macros.append(("RG_A_INS(A)", ", ".join(f'[a{j}] "v"(A[{j}])' for j in range(LL))))
     macros.append(("RG_N_INS(N, C)", ", ".join(f'[n{j}] C(N({j}))' for j in range(LL))))
@@ -156,6 +186,20 @@ def gen(LL, LB):
         bl_in = ', [bl] "v"(bl)' if LL % 2 == 0 else ''  # odd LL: no half-window column, bl unused
         out.append(f'  asm volatile(RG_SQROW_{a} : RG_T_OPS(T) : RG_A_INS(A), [bf] "v"(bf), [bm] "v"(bm){bl_in} : "vcc", "memory");')
         out.append("}")
+    # TPI-1 top-zero dispatchers (rows whose window holds t_{LL-1} write it over the constant 0)
+    out.append(f"template <int a> __device__ __forceinline__ void r27_sqrow_z({sig});")
+    for a in range(LL):
+        out.append(f"template <> __device__ __forceinline__ void r27_sqrow_z<{a}>({sig}) {{")
+        bl_in = ', [bl] "v"(bl)' if LL % 2 == 0 else ''
+        if any(k == LL - 1 for k, _ in window(a)):
+            out.append(f'  asm volatile(RG_SQROZ_{a} : RG_T_OPS_LO(T), [t{LL - 1}] "=&v"(T[{LL - 1}]) : RG_A_INS(A), [bf] "v"(bf), [bm] "v"(bm){bl_in} : "vcc", "memory");')
+        else:
+            out.append(f'  asm volatile(RG_SQROW_{a} : RG_T_OPS_LO(T) : RG_A_INS(A), [bf] "v"(bf), [bm] "v"(bm){bl_in} : "vcc", "memory");')
+        out.append("}")
+    bl_in = ', [bl] "v"(bl)' if LL % 2 == 0 else ''
+    out.append(f"__device__ __forceinline__ void r27_sqrow_f0({sig}) {{")
+    out.append(f'  asm volatile(RG_SQROW_F0 : RG_T_SQ0_OUT(T) : RG_A_INS(A), [bf] "v"(bf), [bm] "v"(bm){bl_in} : "vcc", "memory");')
+    out.append("}")
     out.append("#elif RG_SECTION == 3")
     out.append("template <int TPI, int a> __device__ __forceinline__ void r27f_sqrow(u64 (&T)[LL], const L27& A, u32 bf, u32 bm, u32 bl, const Mod<TPI>& N, u32 np, u32 mk);")
     # TPI 1 (one lane per element: p^2, q^2 and n of <= 1024-bit keys) runs the TPI-4 rows with
