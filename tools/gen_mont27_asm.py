@@ -13,7 +13,10 @@ Each file has sections, picked by RG_SECTION before each #include (mont_engine.i
                             bl at s = W-1 (odd LL needs no half-window column).  See
                             mont_engine.inc mont_sqr for why this covers each limb pair once.
               RGF_ROW / RGF_SQROW_<a>  fused rows (below)
-  2  dispatchers r27_sqrow<a>        (after the limb vector type)
+              RG_OPROW_Z / RG_REDROW_Z / RG_SQROZ_<a>, RG_OPROW_F / RG_SQROW_F0 / RG_REDROW_F0
+                            TPI-1 rows that keep t_{LL-1} logically zero and a product's first
+                            rows over an all-zero accumulator (no 64-bit zero stores)
+  2  dispatchers r27_sqrow<a>, r27_sqrow_z<a>, r27_sqrow_f0   (after the limb vector type)
   3  dispatchers r27f_sqrow<TPI, a>, r27f_row<TPI>  (after Mod)
   4  #undef of every macro of section 1, so the other radix can define them again
 """
