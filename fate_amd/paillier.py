@@ -793,6 +793,23 @@ class CiphertextVector:
     def iupdate(self, other: "CiphertextVector", indexes, stride: int, pk: "PK") -> None:
         """``CiphertextVector::iupdate`` (lib.rs:724-735): data[pos*stride+t] += other[i*stride+t]
         for every position pos listed for sample i, folded per target slot on the device."""
+        if (isinstance(indexes, torch.Tensor) and indexes.dim() == 2 and indexes.numel()
+                and not indexes.is_floating_point() and not indexes.is_complex() and indexes.dtype != torch.bool):
+            # [samples, positions] integer tensor (SecureBoost's bin indexes): the term lists
+            # straight from it, in the reference's sample-major order, in four launches
+            # (sample i's ids are implied: only the positions need a range check)
+            ns, npos = indexes.shape
+            pp = indexes.to(device=self.device).reshape(-1)
+            st = max(int(stride), 1)
+            lo, hi = torch.stack(list(torch.aminmax(pp))).to(torch.int64).tolist()  # one read-back
+            if lo < 0 or (hi + 1) * st > self.count or ns * st > other.count:
+                raise PanicException("index out of bounds")
+            t = torch.arange(st, device=self.device, dtype=torch.int32)
+            slot = torch.add(t, pp.to(torch.int32).view(-1, 1), alpha=st).reshape(-1)
+            base = torch.arange(ns, device=self.device, dtype=torch.int32).view(-1, 1, 1)
+            src = torch.add(t.view(1, 1, -1), base, alpha=st).expand(ns, npos, st).reshape(-1)
+            self._fold_terms(other, src, slot, pk)
+            return
         ii, pp = _flatten_positions(indexes, self.device)
         self._scatter_fold(other, ii, pp, stride, pk)
 
@@ -833,6 +850,11 @@ class CiphertextVector:
         t = torch.arange(stride, device=dev, dtype=torch.int32)
         src = (ii[:, None] * stride + t).reshape(-1)
         slot = (pp[:, None] * stride + t).reshape(-1)
+        self._fold_terms(other, src, slot, pk)
+
+    def _fold_terms(self, other: "CiphertextVector", src: torch.Tensor, slot: torch.Tensor, pk: "PK") -> None:
+        """data[slot[k]] += other[src[k]] for every term k (int32, range-checked by the caller),
+        folded per slot in term order."""
         # one ciphertext per slot (the literal 1 where no term lands: add's identity), then
         # data[s] = add(data[s], fold(terms of s)) for every slot at once
         # the error flags of the fold and of the add are read back once both are queued: no
