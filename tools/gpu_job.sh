@@ -10,7 +10,8 @@
 #                 bench.py --n 131072, the op kernels over tools/bench_legs/ops_pmc_leg.py,
 #                 summarised into gpurun_out/TAG_pmc_encrypt27.json / TAG_pmc_ops.json
 #       sq        SQ / GRBM counter passes over tools/bench_legs/ops_pmc_leg.py (or the leg
-#                 script named by args, e.g. k1024_leg.py), tabled into gpurun_out/TAG_sq.txt
+#                 script named by args, e.g. k1024_leg.py), tabled into gpurun_out/TAG_sq.txt,
+#                 with each dispatch's shader clock in gpurun_out/TAG_clock.txt
 #       evidence  round, then prof, then pmc (the end-of-round record for profiles/)
 #       leg       python tools/bench_legs/ARGS (one bench leg script)
 #       timeline  rocprofv3 kernel trace of tools/bench_legs/hist_leg.py ARGS (PHASES=0), last
@@ -68,6 +69,7 @@ run_sq() {
   pmc_pass sq "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE GRBM_COUNT" python3 $R/tools/bench_legs/$leg "$@"
   pmc_pass sq2 "SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_LDS_BANK_CONFLICT SQ_INSTS_BRANCH" python3 $R/tools/bench_legs/$leg "$@"
   python tools/pmc_sq_compare.py gpurun_out/${T}_sq gpurun_out/${T}_sq2 > gpurun_out/${T}_sq.txt || exit 1
+  python tools/pmc_clock.py gpurun_out/${T}_sq > gpurun_out/${T}_clock.txt || exit 1  # GRBM_GUI_ACTIVE per dispatch
   echo sq_ok
 }
 
