@@ -248,7 +248,85 @@ def valu_roofline(kernel: str, mac32: float, ms: float, hbm_bytes: float, traffi
             "hbm": hbm_block(hbm_bytes, ms, traffic, traffic_source), **extra}
 
 
-def add_kernel_leg(P, pk, a, b, N, stream, dev) -> dict:
+class ClockMeter:
+    """The shader clock a timed leg ran at: fphe_clock_stamp queues one-wave
+    workgroups on the leg's stream just before and just after it; each writes its XCD's
+    shader-clock cycle counter and the constant-rate counter, so (cycles1 - cycles0) /
+    (wall1 - wall0) per XCD is that XCD's mean clock over the leg.  The rooflines price at
+    2.4 GHz; `frac_at_measured_clock` = frac x 2.4 / measured GHz separates a slow box's clock
+    from the code."""
+
+    BLOCKS = 32
+    SLOTS = 256
+
+    def __init__(self, dev, stream):
+        import ctypes
+        from fate_amd import _lib
+        self._c, self._lib = ctypes, _lib
+        self.lib = _lib.load()
+        self.stream = stream
+        self.buf = torch.zeros((self.SLOTS, 3 * self.BLOCKS), dtype=torch.int64, device=dev)
+        self.k = 0
+        self.khz = ctypes.c_uint32(0)
+
+    def stamp(self) -> int:
+        i = self.k % self.SLOTS
+        self.k += 1
+        c = self._c
+        self._lib.check(self.lib.fphe_clock_stamp(c.c_void_p(self.buf[i].data_ptr()), self.BLOCKS, c.byref(self.khz),
+                                                  c.c_void_p(self.stream.cuda_stream)), "fphe_clock_stamp")
+        return i
+
+    def ghz(self, i0: int, i1: int):
+        """Mean shader clock (GHz) between two stamps, over the XCDs seen in both (call after a
+        synchronize); None when the counters give nothing usable."""
+        a = self.buf[i0].view(-1, 3).cpu().tolist()
+        b = self.buf[i1].view(-1, 3).cpu().tolist()
+        first = lambda rows: {int(x): (int(cy), int(w)) for x, cy, w in reversed(rows)}
+        fa, fb = first(a), first(b)
+        per = []
+        for x in sorted(set(fa) & set(fb)):
+            dc = (fb[x][0] - fa[x][0]) & ((1 << 64) - 1)
+            dw = ((fb[x][1] - fa[x][1]) & ((1 << 64) - 1)) / (self.khz.value * 1e3)
+            if dw > 0:
+                per.append(dc / dw / 1e9)
+        if not per or not self.khz.value:
+            return None
+        return {"GHz": round(sum(per) / len(per), 4), "min": round(min(per), 4), "max": round(max(per), 4),
+                "xcds": len(per)}
+
+
+def at_clock(frac: float, clock) -> dict:
+    """frac rescaled to the measured clock (the roofline's peak prices 2.4 GHz)."""
+    if not clock:
+        return {"clock": None, "frac_at_measured_clock": None}
+    return {"clock": clock, "frac_at_measured_clock": round(frac * 2.4 / clock["GHz"], 4)}
+
+
+def timed_reps(fn, reps: int, stream, dev, meter: "ClockMeter") -> dict:
+    """`reps` launches of fn on `stream`, each bracketed by HIP events, queued back to back
+    (timed reps after warm-up), with clock stamps around them all."""
+    evs = []
+    s0 = meter.stamp()
+    for _ in range(reps):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        fn()
+        e1.record(stream)
+        evs.append((e0, e1))
+    s1 = meter.stamp()
+    torch.cuda.synchronize(dev)
+    ms = [a.elapsed_time(b) for a, b in evs]
+    return {"reps": reps, "mean_ms": sum(ms) / len(ms), "min_ms": min(ms), "max_ms": max(ms),
+            "clock": meter.ghz(s0, s1)}
+
+
+def rep_fields(r: dict) -> dict:
+    return {"timed_reps": r["reps"], "kernel_ms_min": round(r["min_ms"], 3), "kernel_ms_max": round(r["max_ms"], 3)}
+
+
+def add_kernel_leg(P, pk, a, b, N, stream, dev, meter=None) -> dict:
     """The ct-add kernel alone (k_add27 through fphe_add_ordered, launched on `stream`) on the
     Hetero-LR-shaped operands, in the exponent-gap order _add computes.  §8(d): an aligned
     add is one mulmod over L = 128 32-bit limbs (32,896 MAC32); each step of exponent gap
@@ -280,16 +358,8 @@ def add_kernel_leg(P, pk, a, b, N, stream, dev) -> dict:
     c1.record(stream)
     for _ in range(5):
         launch()
-    ev = []
-    for _ in range(3):
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        launch()
-        e1.record(stream)
-        ev.append((e0, e1))
-    torch.cuda.synchronize(dev)
-    ms = sum(x.elapsed_time(y) for x, y in ev) / len(ev)
+    reps = timed_reps(launch, 10, stream, dev, meter)
+    ms = reps["mean_ms"]
     L = a.L2
     mac = N * (1 + 4 * float(gaps.double().mean())) * mac32_per_mont(L)
     hist = torch.bincount(gaps.cpu()).tolist()
@@ -309,6 +379,8 @@ def add_kernel_leg(P, pk, a, b, N, stream, dev) -> dict:
                         per_elem_mac32=round(mac / N, 1), gap_histogram=hist, sorted=order is not None)
     blk["cold_kernel_ms"] = round(c0.elapsed_time(c1), 3)
     blk["warmup_launches"] = 6
+    blk.update(rep_fields(reps))
+    blk.update(at_clock(blk["frac"], reps["clock"]))
     blk["issue"] = {"mad64_per_elem": round(mads / N, 1), "achieved": round(mads / (ms / 1e3) / 1e12, 3),
                     "peak": round(PEAK_TMAC32, 3), "unit": "Tmad/s",
                     "frac": round(mads / (ms / 1e3) / 1e12 / PEAK_TMAC32, 4)}
@@ -540,8 +612,11 @@ def main() -> None:
         ct = step()
     barrier()
 
-    # timed region; HIP events on the stream the kernels are launched on
+    # timed region; HIP events on the stream the kernels are launched on, and shader-clock
+    # stamps (fphe_clock_stamp: two one-wave launches, microseconds) around the steps
+    meter = ClockMeter(dev, stream)
     ev_enc = []
+    st_enc0 = meter.stamp()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         pv = coder.encode_f32_vec(xd)
@@ -551,13 +626,29 @@ def main() -> None:
         ct = pk.encrypt_encoded(pv, True)
         e1.record(stream)
         ev_enc.append((e0, e1))
+    st_enc1 = meter.stamp()
     barrier()
     elapsed = time.perf_counter() - t0
+    enc_ms_all = [a.elapsed_time(b) for a, b in ev_enc]
+    enc_kernel_ms = sum(enc_ms_all) / max(len(ev_enc), 1)
+    enc_clock = meter.ghz(st_enc0, st_enc1)
+    per_rank = None
     if dist:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    enc_kernel_ms = sum(a.elapsed_time(b) for a, b in ev_enc) / max(len(ev_enc), 1)
+        # per-rank kernel time and clock: the driver's scaling run can
+        # then tell a rank's imbalance from its box's clock
+        mine = torch.tensor([enc_kernel_ms, enc_clock["GHz"] if enc_clock else float("nan")], dtype=torch.float64,
+                            device=dev)
+        allr = [torch.empty_like(mine) for _ in range(world)]
+        tdist.all_gather(allr, mine)
+        ks = [float(v[0]) for v in allr]
+        cs = [float(v[1]) for v in allr]
+        per_rank = {"encrypt_kernel_ms": [round(v, 3) for v in ks], "clock_GHz": [round(v, 4) for v in cs],
+                    "kernel_ms_min": round(min(ks), 3), "kernel_ms_max": round(max(ks), 3),
+                    "kernel_ms_spread": round(max(ks) / min(ks), 4),
+                    "clock_GHz_min": round(min(cs), 4), "clock_GHz_max": round(max(cs), 4)}
     value = (args.total if strong else world * N) * args.steps / elapsed
 
     # BASELINE config 5's exchange step, outside the timed region: every rank's ciphertext
@@ -614,14 +705,13 @@ def main() -> None:
         ec0.record(stream)
         sk.decrypt_to_encoded(ct)
         ec1.record(stream)
-        e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
+        dec_reps = timed_reps(lambda: sk.decrypt_to_encoded(ct), 5, stream, dev, meter)
         pt = sk.decrypt_to_encoded(ct)
-        e1.record(stream)
         y = coder.decode_f32_vec(pt)
         torch.cuda.synchronize(dev)
-        dec_ms = e0.elapsed_time(e1)
+        dec_ms = dec_reps["mean_ms"]
         dec_cold_ms = ec0.elapsed_time(ec1)  # the first pass: cold clock, growing scratch
+        e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
         xb = x.numpy().view(np.uint32).copy()
         xb[xb == 0x80000000] = 0  # -0.0 encodes to significand 0 -> decodes +0.0 (reference)
         roundtrip_ok = bool(np.array_equal(y.cpu().numpy().view(np.uint32), xb))
@@ -629,12 +719,13 @@ def main() -> None:
         ct2 = pk.encrypt_encoded(coder.encode_f32_vec(torch.flip(xd, [0]) * 0.25), True)
         for _ in range(4):  # untimed: first-call costs of the sort, the output's allocation, the clock
             ct.add(pk, ct2)
-        e0.record(stream)  # no host sync in between (the clock, see the decrypt leg)
+        # the whole add call (order + kernel), 5 reps queued back to back (no gap read-back:
+        # both operands come from the encoder, whose exponent range the kernel covers)
+        add_reps = timed_reps(lambda: ct.add(pk, ct2), 5, stream, dev, meter)
         s = ct.add(pk, ct2)
-        e1.record(stream)
         torch.cuda.synchronize(dev)
-        add_ms = e0.elapsed_time(e1)
-        add_kernel = add_kernel_leg(P, pk, ct, ct2, N, stream, dev)
+        add_ms = add_reps["mean_ms"]
+        add_kernel = add_kernel_leg(P, pk, ct, ct2, N, stream, dev, meter)
         # end-to-end from host f32 to the reference's signed ciphertext integers in pinned host
         # memory (export out of the Montgomery-resident form included), one pass
         xh = x.pin_memory()
@@ -647,7 +738,42 @@ def main() -> None:
         sh = neg_e.cpu(); eh = exp_e.cpu()
         torch.cuda.synchronize(dev)
         e2e = time.perf_counter() - t0
-        del mag_e, neg_e, exp_e
+        del mag_e, neg_e, exp_e, Ch
+        # ... and to the bytes that leave the party: the reference's pickle
+        # state of the vector, bincode(CiphertextVector) of the signed integers
+        # (paillier.rs:219-226), formatted on the device (fate_amd.wire) and copied into a
+        # pinned host buffer -- what the federation transport sends
+        from fate_amd import wire
+        wire_cap = 8 + N * (4 + 8 + 4 + 1 + 8 * ct.L2)  # the widest record: a full-width hex integer
+        Wh = torch.empty(wire_cap, dtype=torch.uint8, pin_memory=True)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        cw = pk.encrypt_encoded(coder.encode_f32_vec(xh.to(dev, non_blocking=True)), True)
+        whead, wrec = wire.ciphertext_vector_records(cw, pk)
+        Wh[8:8 + wrec.numel()].copy_(wrec, non_blocking=True)
+        torch.cuda.synchronize(dev)
+        e2e_wire = time.perf_counter() - t0
+        Wh[:8] = torch.frombuffer(bytearray(whead), dtype=torch.uint8)
+        wire_bytes = 8 + wrec.numel()
+        # the wire step alone (export + format + D2H), on the same vector
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        whead, wrec = wire.ciphertext_vector_records(cw, pk)
+        Wh[8:8 + wrec.numel()].copy_(wrec, non_blocking=True)
+        torch.cuda.synchronize(dev)
+        wire_only = time.perf_counter() - t0
+        # round trip of a sample of the bytes through the host parser (the reference's layout)
+        nchk = min(N, 4096)
+        hchk, rchk = wire.ciphertext_vector_records(cw._gather(torch.arange(nchk)), pk)
+        back, used = wire.ciphertext_vector_from_bincode(hchk + bytes(rchk.cpu().numpy()), pk)
+        wire_ok = used == 8 + rchk.numel() and torch.equal(back.C[: (nchk + 63) // 64], cw.C[: (nchk + 63) // 64]) \
+            and torch.equal(back.sign[:nchk], cw.sign[:nchk]) and torch.equal(back.exp[:nchk], cw.exp[:nchk])
+        e2e_wire_block = {"encrypts_per_s": round(N / e2e_wire, 1), "seconds": round(e2e_wire, 4),
+                          "wire_bytes": int(wire_bytes), "wire_only_s": round(wire_only, 4),
+                          "wire_only_GBps": round(wire_bytes / wire_only / 1e9, 3), "sample_round_trip_ok": bool(wire_ok),
+                          "scope": "host f32 (pinned) -> H2D -> device encode + obfuscated encrypt -> export of the "
+                                   "signed integers -> device bincode formatting -> D2H into pinned host bytes"}
+        del cw, wrec, Wh, back
         # ct x pt (SecureBoost GOSS-style weights; negatives take the device inverse branch)
         gw = torch.Generator().manual_seed(777 + rank)
         wts = (torch.rand(N, generator=gw, dtype=torch.float32) * 3.0 - 1.0).to(dev)
@@ -658,11 +784,10 @@ def main() -> None:
         ec0.record(stream)
         ct.mul(pk, pw)  # untimed: grows the context scratch to the op's size (and warms the clock)
         ec1.record(stream)
-        e0.record(stream)  # queued right behind it (see the decrypt leg)
+        mul_reps = timed_reps(lambda: ct.mul(pk, pw), 5, stream, dev, meter)
         m = ct.mul(pk, pw)
-        e1.record(stream)
         torch.cuda.synchronize(dev)
-        mul_ms = e0.elapsed_time(e1)
+        mul_ms = mul_reps["mean_ms"]
         mul_cold_ms = ec0.elapsed_time(ec1)
         # SecureBoost histogram (BASELINE config 4 shape at one GPU): (g, h) interleaved with
         # stride 2, HF features x 32 bins, iupdate = per-bin ct-add fold on the device
@@ -687,10 +812,13 @@ def main() -> None:
             P.CiphertextVector.zeros(HF * NB * 2, pk._key.L2, dev).iupdate(src, positions_d, 2, pk)
             hh = P.CiphertextVector.zeros(HF * NB * 2, pk._key.L2, dev)
             torch.cuda.synchronize(dev)
+            s0h = meter.stamp()
             t0h = time.perf_counter()
             hh.iupdate(src, positions_d, 2, pk)
+            s1h = meter.stamp()
             torch.cuda.synchronize(dev)
             secs = time.perf_counter() - t0h
+            hist_clock.append(meter.ghz(s0h, s1h))
             # property check: decrypted bins == float64 sums of the encoded inputs
             hd = coder.decode_f64_vec(sk.decrypt_to_encoded(hh)).cpu().reshape(HF * NB, 2)
             want = torch.zeros(HF * NB, 2, dtype=torch.float64)
@@ -700,6 +828,7 @@ def main() -> None:
             fin = torch.isfinite(want)
             return hh, secs, bool(torch.allclose(hd[fin], want[fin], rtol=1e-9, atol=1e-6)), want
 
+        hist_clock = []
         hist, hist_s, hist_ok, want = run_hist(gh, g_sb.double(), h_sb.double())
         hist_h = P.CiphertextVector.zeros(HF * NB * 2, pk._key.L2, dev)
         torch.cuda.synchronize(dev)
@@ -709,20 +838,24 @@ def main() -> None:
         hist_host_s = time.perf_counter() - t0h
         del hist_h
         iupdate_block = iupdate_roofline(gh, positions, 2, HF * NB * 2, hist_s, key_bits)
+        iupdate_block.update(at_clock(iupdate_block["frac"], hist_clock[0]))
         # the same call 5 times back to back (no host sync between calls; each still reads
         # back its own small bookkeeping): the shader clock ramps up over the first ~25 ms of
         # a full-chip burst (profiles/r04/r04j2_clock_probe.txt), so one cold 18-ms call runs
         # below the clock a busy pipeline sees.  Reported beside, `frac` stays the cold call's.
         hs5 = [P.CiphertextVector.zeros(HF * NB * 2, pk._key.L2, dev) for _ in range(5)]
         torch.cuda.synchronize(dev)
+        s0h = meter.stamp()
         t0h = time.perf_counter()
         for h5 in hs5:
             h5.iupdate(gh, positions_d, 2, pk)
+        s1h = meter.stamp()
         torch.cuda.synchronize(dev)
         sus_s = (time.perf_counter() - t0h) / 5
         del hs5
-        iupdate_block["sustained"] = {"calls": 5, "mean_s": round(sus_s, 5),
-                                      "frac": iupdate_roofline(gh, positions, 2, HF * NB * 2, sus_s, key_bits)["frac"]}
+        sus_frac = iupdate_roofline(gh, positions, 2, HF * NB * 2, sus_s, key_bits)["frac"]
+        iupdate_block["sustained"] = {"calls": 5, "mean_s": round(sus_s, 5), "frac": sus_frac,
+                                      **at_clock(sus_frac, meter.ghz(s0h, s1h))}
         # the same fold over the encrypt leg's vector and its mirror (x with the edge values
         # 0, +-1e-30, +-3.4e38 among the first inputs): exponent gaps up to 31 force one
         # 124-squaring alignment chain, a ~4.8 ms critical path on a single wave
@@ -776,21 +909,21 @@ def main() -> None:
         # allocated there, not in the timed calls
         # (timed passes queued behind them with no host sync: the clock, see the decrypt leg)
         sk1.decrypt_to_encoded(pk1.encrypt_encoded(pv1, True))
-        e0.record(stream)
+        enc1 = timed_reps(lambda: pk1.encrypt_encoded(pv1, True), 5, stream, dev, meter)
         c1 = pk1.encrypt_encoded(pv1, True)
-        e1.record(stream)
-        e2 = torch.cuda.Event(enable_timing=True); e3 = torch.cuda.Event(enable_timing=True)
-        e2.record(stream)
+        dec1 = timed_reps(lambda: sk1.decrypt_to_encoded(c1), 5, stream, dev, meter)
         d1 = sk1.decrypt_to_encoded(c1)
-        e3.record(stream)
         torch.cuda.synchronize(dev)
-        enc1_ms = e0.elapsed_time(e1)
-        dec1_ms = e2.elapsed_time(e3)
+        enc1_ms, dec1_ms = enc1["mean_ms"], dec1["mean_ms"]
+        e2 = torch.cuda.Event(enable_timing=True); e3 = torch.cuda.Event(enable_timing=True)
         y1 = coder1.decode_f32_vec(d1)
+        ef1 = round(N * enc_mac32_per_elem(1024) / (enc1_ms / 1e3) / 1e12 / PEAK_TMAC32, 4)
+        df1 = round(N * dec_mac32_per_elem(1024) / (dec1_ms / 1e3) / 1e12 / PEAK_TMAC32, 4)
         k1024 = {"encrypt_per_s": round(N / (enc1_ms / 1e3), 1), "decrypt_per_s": round(N / (dec1_ms / 1e3), 1),
                  "roundtrip_bit_exact": bool(np.array_equal(y1.cpu().numpy().view(np.uint32), xb)),
-                 "encrypt_roofline_frac": round(N * enc_mac32_per_elem(1024) / (enc1_ms / 1e3) / 1e12 / PEAK_TMAC32, 4),
-                 "decrypt_roofline_frac": round(N * dec_mac32_per_elem(1024) / (dec1_ms / 1e3) / 1e12 / PEAK_TMAC32, 4)}
+                 "encrypt_roofline_frac": ef1, "decrypt_roofline_frac": df1,
+                 "encrypt_reps": {**rep_fields(enc1), **at_clock(ef1, enc1["clock"])},
+                 "decrypt_reps": {**rep_fields(dec1), **at_clock(df1, dec1["clock"])}}
         del c1, d1, y1, pv1
         # 4096-bit keys (the TPI-8 geometry; he_param.key_length is a job parameter): rates on
         # the first 2^16 elements (a 4096-bit encrypt is ~8x a 2048-bit one), round trip
@@ -859,6 +992,8 @@ def main() -> None:
             "decrypt_per_s": round(N / (dec_ms / 1e3), 1),
             "ct_add_per_s": round(N / (add_ms / 1e3), 1),
             "e2e_host_encrypts_per_s": round(N / e2e, 1),
+            "e2e_wire_bytes": e2e_wire_block,
+            "ct_add_reps": rep_fields(add_reps),
             "roundtrip_bit_exact": roundtrip_ok,
             "decrypt_roofline_frac": round(N * dec_mac32_per_elem(key_bits) / (dec_ms / 1e3) / 1e12 / PEAK_TMAC32, 4),
             "rooflines": {
@@ -866,7 +1001,7 @@ def main() -> None:
                                          N * dec_mac32_per_elem(key_bits), dec_ms,
                                          N * (key_bits // 4 + 4 + key_bits // 8),
                                          traffic=_traffic("decrypt", N), traffic_source=pmc_ops_traffic("decrypt")[1],
-                                         cold_kernel_ms=round(dec_cold_ms, 3)),
+                                         cold_kernel_ms=round(dec_cold_ms, 3), **rep_fields(dec_reps)),
                 "iupdate": iupdate_block,
                 "ct_add": add_kernel,
                 # §8(d): float significands (E = 56): (56 + 12 + 16) mulmods over L = 128, + 3
@@ -876,10 +1011,12 @@ def main() -> None:
                                         (N * (56 + 12 + 16) + 3 * n_neg) * mac32_per_mont(key_bits // 16), mul_ms,
                                         N * 2 * (key_bits // 4 + 5) + N * 13, traffic=_traffic("ct_mul", N),
                                         traffic_source=pmc_ops_traffic("ct_mul")[1], negative_weights=n_neg,
-                                        cold_kernel_ms=round(mul_cold_ms, 3)),
+                                        cold_kernel_ms=round(mul_cold_ms, 3), **rep_fields(mul_reps)),
             },
         }
-        del pt, y, ct2, s, ce, Ch, m, gh, hist
+        for _k, _r in (("decrypt", dec_reps), ("ct_mul", mul_reps)):
+            extras["rooflines"][_k].update(at_clock(extras["rooflines"][_k]["frac"], _r["clock"]))
+        del pt, y, ct2, s, ce, m, gh, hist
         # BASELINE config 4 at its stated size (10M samples x 10 features x 32 bins, 2048-bit):
         # unpacked ct x pt + the 200M-term iupdate, packed iupdate + cumsum + squeeze, sharded
         # over the ranks with the cross-rank fold (tools/bench_legs/secureboost_full.py)
@@ -924,7 +1061,9 @@ def main() -> None:
         "issue": {"mad64_per_elem": enc_mad27_per_elem(key_bits, pk.n), "achieved": round(mad27, 3),
                   "peak": round(PEAK_TMAC32, 3), "unit": "Tmad/s", "frac": round(mad27 / PEAK_TMAC32, 4)},
         "hbm": hbm_block(hbm_bytes, enc_kernel_ms, round(tb * N) if tb is not None else None, tsrc),
+        "kernel_ms_per_step": [round(v, 3) for v in enc_ms_all],
     }
+    roofline.update(at_clock(roofline["frac"], enc_clock))
     out = {
         "metric": "Paillier-2048 encrypts/sec device-resident",
         "value": round(value, 1),
@@ -946,6 +1085,8 @@ def main() -> None:
                     "obfuscate": True, "parallelism": f"shard{world}"}),
         "roofline": roofline,
     }
+    if per_rank is not None:
+        out["per_rank"] = per_rank
     out.update(gather_info)
     out.update(extras)
     if world == 1 and not args.no_cpu_baseline and not strong:

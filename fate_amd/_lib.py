@@ -38,6 +38,7 @@ EXPORTED_SYMBOLS = (
     "fphe_encrypt", "fphe_encrypt_crt", "fphe_decrypt", "fphe_add", "fphe_add_ordered", "fphe_add_order", "fphe_mul", "fphe_neg", "fphe_sqmul", "fphe_align",
     "fphe_fold", "fphe_fold_segments", "fphe_permute", "fphe_export_signed", "fphe_import_signed",
     "fphe_wire_lengths", "fphe_wire_encode", "fphe_wire_scan", "fphe_wire_decode", "fphe_chacha20_blocks",
+    "fphe_clock_stamp",
 )
 
 _lock = threading.Lock()
@@ -130,6 +131,8 @@ def load() -> ctypes.CDLL:
         sz = ctypes.c_size_t
         lib.fphe_chacha20_blocks.argtypes = [vp, ctypes.c_uint32, vp, sz, vp, vp]
         lib.fphe_chacha20_blocks.restype = st
+        lib.fphe_clock_stamp.argtypes = [vp, ctypes.c_uint32, vp, vp]
+        lib.fphe_clock_stamp.restype = st
         lib.fphe_wire_lengths.argtypes = [vp, vp, ctypes.c_uint32, sz, vp, vp, vp]
         lib.fphe_wire_encode.argtypes = [vp, vp, vp, ctypes.c_uint32, sz, vp, vp, vp, vp, vp]
         lib.fphe_wire_scan.argtypes = [vp, sz, sz, sz, vp, vp, vp, vp, vp, vp]

@@ -2203,18 +2203,27 @@ fphe_status fphe_export_signed(fphe_ctx* c, const uint32_t* C, const uint8_t* si
   std::lock_guard<std::mutex> lk(c->mu);
   DevGuard g(c->device);
   hipStream_t s = (hipStream_t)stream;
-  // out of the Montgomery-resident form into a stream-ordered scratch vector, then the
-  // reference's signed integers
+  // out of the Montgomery-resident form into a stream-ordered scratch of at most
+  // kExportSpan elements, then the reference's signed integers, span by span: peak memory is
+  // the vector, the magnitudes and ~0.5 GB (at 2048 bits), not a second copy of the vector
+  // (config 5's 100M-element vectors are ~52 GB each)
+  constexpr size_t kExportSpan = (size_t)1 << 20;  // whole tiles
+  const size_t span = count < kExportSpan ? count : kExportSpan;
   CallBufs B(s);
-  u32* plain = B.get<u32>((size_t)ntiles_of(count) * c->L2 * FPHE_WAVE);
+  u32* plain = B.get<u32>((size_t)ntiles_of(span) * c->L2 * FPHE_WAVE);
   if (!B.ok) return FPHE_ERR_HIP;
-  fphe_status st = c->L2 == 256   ? launch_mont_const27<256>(c, C, count, nullptr, plain, s)
-                   : c->L2 == 128 ? launch_mont_const27<128>(c, C, count, nullptr, plain, s)
-                                  : launch_mont_const27<64>(c, C, count, nullptr, plain, s);
-  if (st != FPHE_OK) return st;
-  hipLaunchKernelGGL(k_export_signed, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, s, c->K.N2, (u32)c->L2,
-                     plain, sign, count, mag, neg);
-  return hip_ok(hipGetLastError());
+  for (size_t e0 = 0; e0 < count; e0 += span) {
+    const size_t m = count - e0 < span ? count - e0 : span;
+    const uint32_t* Cs = C + (e0 / FPHE_WAVE) * c->L2 * FPHE_WAVE;
+    fphe_status st = c->L2 == 256   ? launch_mont_const27<256>(c, Cs, m, nullptr, plain, s)
+                     : c->L2 == 128 ? launch_mont_const27<128>(c, Cs, m, nullptr, plain, s)
+                                    : launch_mont_const27<64>(c, Cs, m, nullptr, plain, s);
+    if (st != FPHE_OK) return st;
+    hipLaunchKernelGGL(k_export_signed, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, c->K.N2, (u32)c->L2,
+                       plain, sign + e0, m, mag + e0 * c->L2, neg + e0);
+    if (hipGetLastError() != hipSuccess) return FPHE_ERR_HIP;
+  }
+  return FPHE_OK;
 }
 
 fphe_status fphe_import_signed(fphe_ctx* c, const uint32_t* mag, const uint8_t* neg, size_t count, uint32_t* C,
@@ -2304,6 +2313,35 @@ fphe_status fphe_wire_decode(const uint8_t* buf, const int64_t* dig_off, const i
   const size_t threads = count * L;
   hipLaunchKernelGGL(k_wire_decode, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, (hipStream_t)stream, buf,
                      dig_off, dig_len, radix, L, count, mag, err);
+  return hip_ok(hipGetLastError());
+}
+
+// Shader-clock stamps (diagnostics; bench.py's per-leg clock).  `blocks`
+// one-wave workgroups, dealt round-robin over the XCDs by the dispatcher; lane 0 of block b
+// writes {XCC id, shader-clock counter (clock64: s_memtime, counts SCLK cycles), constant-rate
+// counter (wall_clock64)} to out[3b .. 3b+2] with vector stores.  Two stamps queued on the
+// stream around a launch give each XCD's mean shader clock over it (the counters of different
+// XCDs are not synchronised, so the host pairs stamps by XCC id).
+__global__ __launch_bounds__(64) void k_clock_stamp(unsigned long long* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long c = clock64();
+  const unsigned long long w = wall_clock64();
+  const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 15u;  // HW_REG_XCC_ID
+  out[3 * blockIdx.x] = xcc;
+  out[3 * blockIdx.x + 1] = c;
+  out[3 * blockIdx.x + 2] = w;
+}
+
+fphe_status fphe_clock_stamp(uint64_t* out, uint32_t blocks, uint32_t* wall_khz, void* stream) {
+  if (!out || blocks == 0 || blocks > 1024) return FPHE_ERR_ARG;
+  if (wall_khz) {
+    int dev = 0, khz = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess)
+      return FPHE_ERR_HIP;
+    *wall_khz = (uint32_t)khz;
+  }
+  hipLaunchKernelGGL(k_clock_stamp, dim3(blocks), dim3(64), 0, (hipStream_t)stream, (unsigned long long*)out);
   return hip_ok(hipGetLastError());
 }
 

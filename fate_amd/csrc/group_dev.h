@@ -496,7 +496,10 @@ __global__ __launch_bounds__(kGrBlock) void k_gr_gapsel(const int32_t* __restric
     const int32_t jmin = gr_seg_jmin<L>(c, off, s, NE, ord, Src, ssign, one);
     for (int32_t j = jmin + (G > gmin ? G : gmin); j < NE; ++j) {
       const int32_t g = j - jmin;
-      if (c[j] == 0 || raise_cost(g) > xmax) continue;
+      // k_segfold27 squares a raised partial at most 4 kMaxGap times: a larger gap (crafted
+      // exponents only, reachable under FPHE_FOLD_RAISE=force) stays in the exponent merge,
+      // whose alignment flags FPHE_EF_EXP_RANGE and refolds exactly
+      if (c[j] == 0 || g > kMaxGap || raise_cost(g) > xmax) continue;
       if (hist) {
         const long long cap = r0 - raise_cost(g) > 1 ? r0 - raise_cost(g) : 1;
         const int32_t gi = g < kGapHist ? g : kGapHist - 1;

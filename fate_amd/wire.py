@@ -168,15 +168,16 @@ def plaintext_vector_from_bincode(buf: bytes, device=None) -> PlaintextVector:
 
 
 # ---- ciphertext vectors, on the device --------------------------------------------------
-def ciphertext_vector_to_bincode(cv: CiphertextVector, pk: Optional[PK] = None) -> bytes:
-    """``CiphertextVector {data: Vec<Ciphertext {significant_encryped, exp}>}``
-    (fixedpoint_paillier/src/lib.rs:237-241,353-356) of the reference's signed integers
-    (under ``pk``, else the key the vector carries)."""
+def ciphertext_vector_records(cv: CiphertextVector, pk: Optional[PK] = None) -> Tuple[bytes, torch.Tensor]:
+    """The bincode of ``cv`` as (the 8-byte length header, the records as a DEVICE uint8
+    tensor): each record is ``Ciphertext {significant_encryped, exp}`` of the reference's signed
+    integer (under ``pk``, else the key the vector carries), formatted on the device.  The
+    caller moves the records to where they go (a pinned buffer, the transport)."""
     n = cv.count
     head = struct.pack("<Q", n)
-    if n == 0:
-        return head
     dev = cv.device
+    if n == 0:
+        return head, torch.empty(0, dtype=torch.uint8, device=dev)
     lib = _lib.load()
     mag, neg, exp = cv.export_signed(pk) if pk is not None else cv.signed_rows()
     L = int(mag.shape[1])
@@ -191,7 +192,17 @@ def ciphertext_vector_to_bincode(cv: CiphertextVector, pk: Optional[PK] = None) 
     exp = exp.to(torch.int32).contiguous()
     _lib.check(lib.fphe_wire_encode(_ptr(mag), _ptr(neg), _ptr(exp), L, n, _ptr(rec_off), _ptr(rec_len), _ptr(radix),
                                     _ptr(out), s), "fphe_wire_encode")
-    res = bytearray(8 + total)
+    return head, out
+
+
+def ciphertext_vector_to_bincode(cv: CiphertextVector, pk: Optional[PK] = None) -> bytes:
+    """``CiphertextVector {data: Vec<Ciphertext {significant_encryped, exp}>}``
+    (fixedpoint_paillier/src/lib.rs:237-241,353-356) of the reference's signed integers
+    (under ``pk``, else the key the vector carries)."""
+    head, out = ciphertext_vector_records(cv, pk)
+    if out.numel() == 0:
+        return head
+    res = bytearray(8 + out.numel())
     res[:8] = head
     torch.from_numpy(np.frombuffer(res, dtype=np.uint8)[8:]).copy_(out)  # D2H straight into the result
     return bytes(res)

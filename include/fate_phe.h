@@ -283,7 +283,9 @@ fphe_status fphe_permute(const uint32_t* Cin, const uint8_t* sin, const int32_t*
  * and neg[count] (1 = negative), one Montgomery product per element out of M(.); the wire /
  * pickle path and parity checks use this (CiphertextVector.__getstate__, paillier.rs:219-226).
  * import: the inverse, for |value| < n^2 (c = n^2 - |value| for a negative value), one
- * product into M(.). */
+ * product into M(.).  Device memory beyond the caller's buffers: export works through a
+ * stream-ordered scratch of at most 2^20 elements (0.5 GB at 2048 bits) whatever the count;
+ * import converts in place. */
 fphe_status fphe_export_signed(fphe_ctx* ctx, const uint32_t* C, const uint8_t* sign, size_t count, uint32_t* mag,
                                uint8_t* neg, void* stream);
 fphe_status fphe_import_signed(fphe_ctx* ctx, const uint32_t* mag, const uint8_t* neg, size_t count, uint32_t* C,
@@ -325,6 +327,14 @@ fphe_status fphe_wire_decode(const uint8_t* buf, const int64_t* dig_off, const i
  * nonce = {e mod 2^32, call nonce hi, call nonce lo}. */
 fphe_status fphe_chacha20_blocks(const uint32_t key[8], uint32_t counter, const uint32_t nonce[3], size_t nblocks,
                                  uint32_t* out, void* stream);
+
+/* Diagnostics: shader-clock stamps (not part of the reference's surface; bench.py reports the
+ * clock each timed leg ran at).  Queues `blocks` (1..1024) one-wave workgroups on `stream`;
+ * block b writes out[3b] = its XCC (XCD) id, out[3b+1] = the shader-clock cycle counter,
+ * out[3b+2] = the constant-rate counter, whose rate in kHz goes to *wall_khz when non-NULL.
+ * out is a DEVICE buffer of 3*blocks uint64.  (c1 - c0) / (w1 - w0) * wall_khz * 1e3 over two
+ * stamps of the same XCD is that XCD's mean clock between them. */
+fphe_status fphe_clock_stamp(uint64_t* out, uint32_t blocks, uint32_t* wall_khz, void* stream);
 
 #ifdef __cplusplus
 }

@@ -194,6 +194,204 @@ int gref_tdiv_r(const char* a_hex, const char* m_hex, char* out, size_t cap) {
   return 0;
 }
 
+/* ---------------- bulk vector checkers (binary, threaded) ----------------
+ * Every vector crosses this interface as the reference's signed integers: element i is the
+ * magnitude in L little-endian uint32 words at w[i*L], a negative flag neg[i] and the base-16
+ * exponent exp[i] (the device's fphe_export_signed layout).  The ops are the reference's
+ * sequential loops, element by element, on libgmp (the library rug wraps):
+ *   gref_fold     iupdate / intervals_sum / matmul's add_assign loop (lib.rs:724-791, 861-908):
+ *                 acc[slot[k]] = Ciphertext::add(acc[slot[k]], src[term[k]]) for k ascending
+ *   gref_mul      Ciphertext::mul (lib.rs:334-349), both branches and the panic
+ *   gref_squeeze  CiphertextVector::pack_squeeze (lib.rs:439-450)
+ *   gref_cumsum   CiphertextVector::chunking_cumsum_with_step (lib.rs:760-771)
+ * Slots (fold) or elements (mul) are split over `threads` pthreads; each thread owns its slots
+ * outright, so the per-slot term order is the reference's. */
+extern void __gmpz_import(mpz_struct*, size_t, int, size_t, int, size_t, const void*);
+extern void* __gmpz_export(void*, size_t*, int, size_t, int, size_t, const mpz_struct*);
+extern void __gmpz_neg(mpz_struct*, const mpz_struct*);
+extern int __gmpz_cmp(const mpz_struct*, const mpz_struct*);
+extern int __gmpz_cmp_ui(const mpz_struct*, unsigned long);
+extern void __gmpz_tdiv_q_2exp(mpz_struct*, const mpz_struct*, unsigned long);
+
+static void ld_ct(mpz_struct* z, const uint32_t* w, int L, int neg) {
+  __gmpz_import(z, (size_t)L, -1, 4, 0, 0, w);
+  if (neg) __gmpz_neg(z, z);
+}
+/* returns -1 when |z| needs more than L words (never for values < n^2 at the key's L) */
+static int st_ct(uint32_t* w, int L, uint8_t* neg, const mpz_struct* z) {
+  size_t cnt = 0;
+  memset(w, 0, 4u * (size_t)L);
+  if (SGN(z) != 0) {
+    const size_t bits = (size_t)(z->_mp_size < 0 ? -z->_mp_size : z->_mp_size) * 64u;
+    if (bits > 32u * (size_t)L + 64u) return -1;
+    uint32_t tmp[4096 / 32 * 2 + 4];
+    __gmpz_export(tmp, &cnt, -1, 4, 0, 0, z);
+    if (cnt > (size_t)L) return -1;
+    memcpy(w, tmp, 4u * cnt);
+  }
+  *neg = SGN(z) < 0;
+  return 0;
+}
+static int is_literal_one(const mpz_struct* z) { return z->_mp_size == 1 && z->_mp_d[0] == 1; }
+static void fp_add_into(gref_ctx* c, mpz_struct* acc, int* ae, const mpz_struct* tc, int te, mpz_struct* t,
+                        mpz_struct* e16);
+
+typedef struct {
+  gref_ctx* c; int L; int tid, threads; int rc;
+  const uint32_t* sw; const uint8_t* sn; const int32_t* se;
+  const int64_t* term; const int64_t* slot; long nterms; long nslots;
+  uint32_t* aw; uint8_t* an; int32_t* ae;
+} fold_job;
+
+static void* fold_worker(void* arg) {
+  fold_job* j = (fold_job*)arg;
+  const long nown = (j->nslots - j->tid + j->threads - 1) / j->threads;
+  mpz_struct* acc = (mpz_struct*)calloc(nown > 0 ? nown : 1, sizeof(mpz_struct));
+  int* ae = (int*)calloc(nown > 0 ? nown : 1, sizeof(int));
+  mpz_t term, t, e16;
+  __gmpz_init(term); __gmpz_init(t); __gmpz_init(e16);
+  for (long s = j->tid, k = 0; s < j->nslots; s += j->threads, ++k) {
+    __gmpz_init(&acc[k]);
+    ld_ct(&acc[k], j->aw + (size_t)s * j->L, j->L, j->an[s]);
+    ae[k] = j->ae[s];
+  }
+  for (long k = 0; k < j->nterms; ++k) {
+    const long s = (long)j->slot[k];
+    if (s % j->threads != j->tid) continue;
+    const long i = (long)j->term[k];
+    ld_ct(term, j->sw + (size_t)i * j->L, j->L, j->sn[i]);
+    mpz_struct* a = &acc[s / j->threads];
+    int* e = &ae[s / j->threads];
+    /* add(a, b): a literal 1 returns b, then b literal 1 returns a (lib.rs:303-308) */
+    if (!is_literal_one(a) && is_literal_one(term)) continue;
+    fp_add_into(j->c, a, e, term, j->se[i], t, e16);
+  }
+  for (long s = j->tid, k = 0; s < j->nslots; s += j->threads, ++k) {
+    if (st_ct(j->aw + (size_t)s * j->L, j->L, j->an + s, &acc[k])) j->rc = -1;
+    j->ae[s] = ae[k];
+    __gmpz_clear(&acc[k]);
+  }
+  free(acc); free(ae);
+  __gmpz_clear(term); __gmpz_clear(t); __gmpz_clear(e16);
+  return NULL;
+}
+
+/* acc (nslots elements, in/out: the target vector's current state) += the listed terms */
+int gref_fold(gref_ctx* c, int L, const uint32_t* sw, const uint8_t* sn, const int32_t* se, const int64_t* term,
+              const int64_t* slot, long nterms, uint32_t* aw, uint8_t* an, int32_t* ae, long nslots, int threads) {
+  if (threads < 1) threads = 1;
+  pthread_t th[64];
+  fold_job jobs[64];
+  if (threads > 64) threads = 64;
+  for (int t = 0; t < threads; ++t) {
+    fold_job j = {c, L, t, threads, 0, sw, sn, se, term, slot, nterms, nslots, aw, an, ae};
+    jobs[t] = j;
+    pthread_create(&th[t], NULL, fold_worker, &jobs[t]);
+  }
+  int rc = 0;
+  for (int t = 0; t < threads; ++t) { pthread_join(th[t], NULL); rc |= jobs[t].rc; }
+  return rc;
+}
+
+typedef struct {
+  gref_ctx* c; int L, Lp; int tid, threads; int rc;
+  const uint32_t* sw; const uint8_t* sn; const int32_t* se;
+  const uint32_t* pw; const uint8_t* pn; const int32_t* pe; long n;
+  uint32_t* ow; uint8_t* on; int32_t* oe;
+} mul_job;
+
+static void* mul_worker(void* arg) {
+  mul_job* j = (mul_job*)arg;
+  mpz_t ct, b, r, t, maxint, big;
+  __gmpz_init(ct); __gmpz_init(b); __gmpz_init(r); __gmpz_init(t); __gmpz_init(maxint); __gmpz_init(big);
+  __gmpz_tdiv_q_2exp(maxint, j->c->n, 1);   /* max_int = n / 2 (lib.rs:408-413) */
+  __gmpz_sub(big, j->c->n, maxint);         /* n - max_int */
+  for (long i = j->tid; i < j->n; i += j->threads) {
+    ld_ct(ct, j->sw + (size_t)i * j->L, j->L, j->sn[i]);
+    ld_ct(b, j->pw + (size_t)i * j->Lp, j->Lp, j->pn[i]);
+    if (__gmpz_cmp(big, b) <= 0) {          /* large plaintext: invert(c)^(n - b) */
+      if (!__gmpz_invert(t, ct, j->c->ns)) { j->rc = -2; continue; }
+      __gmpz_sub(r, j->c->n, b);
+      __gmpz_powm(r, t, r, j->c->ns);
+    } else if (__gmpz_cmp(b, maxint) <= 0) { /* c^b (a negative b inverts inside powm) */
+      if (SGN(b) < 0 && !__gmpz_invert(t, ct, j->c->ns)) { j->rc = -2; continue; }
+      __gmpz_powm(r, ct, b, j->c->ns);
+    } else {
+      j->rc = -3;                           /* panic!("invalid plaintext") */
+      continue;
+    }
+    if (st_ct(j->ow + (size_t)i * j->L, j->L, j->on + i, r)) j->rc = -1;
+    j->oe[i] = j->se[i] + j->pe[i];
+  }
+  __gmpz_clear(ct); __gmpz_clear(b); __gmpz_clear(r); __gmpz_clear(t); __gmpz_clear(maxint); __gmpz_clear(big);
+  return NULL;
+}
+
+/* out[i] = Ciphertext::mul(src[i], pt[i]); pt significands signed (Lp words + negative flag) */
+int gref_mul(gref_ctx* c, int L, const uint32_t* sw, const uint8_t* sn, const int32_t* se, int Lp, const uint32_t* pw,
+             const uint8_t* pn, const int32_t* pe, long n, uint32_t* ow, uint8_t* on, int32_t* oe, int threads) {
+  if (threads < 1) threads = 1;
+  if (threads > 64) threads = 64;
+  pthread_t th[64];
+  mul_job jobs[64];
+  for (int t = 0; t < threads; ++t) {
+    mul_job j = {c, L, Lp, t, threads, 0, sw, sn, se, pw, pn, pe, n, ow, on, oe};
+    jobs[t] = j;
+    pthread_create(&th[t], NULL, mul_worker, &jobs[t]);
+  }
+  int rc = 0;
+  for (int t = 0; t < threads; ++t) { pthread_join(th[t], NULL); if (jobs[t].rc) rc = jobs[t].rc; }
+  return rc;
+}
+
+/* pack_squeeze: per chunk of pack_num, acc = x0; acc = powm(acc, 2^shift) * y tdiv n^2 */
+int gref_squeeze(gref_ctx* c, int L, const uint32_t* sw, const uint8_t* sn, long n, int pack_num,
+                 unsigned long shift_bit, uint32_t* ow, uint8_t* on, int32_t* oe) {
+  mpz_t acc, y, base, t;
+  __gmpz_init(acc); __gmpz_init(y); __gmpz_init(base); __gmpz_init(t);
+  __gmpz_set_ui(base, 1);
+  __gmpz_mul_2exp(base, base, shift_bit);
+  int rc = 0;
+  for (long h = 0, o = 0; h < n; h += pack_num, ++o) {
+    ld_ct(acc, sw + (size_t)h * L, L, sn[h]);
+    for (long k = h + 1; k < h + pack_num && k < n; ++k) {
+      __gmpz_powm(acc, acc, base, c->ns);
+      ld_ct(y, sw + (size_t)k * L, L, sn[k]);
+      __gmpz_mul(t, acc, y);
+      __gmpz_tdiv_r(acc, t, c->ns);
+    }
+    if (st_ct(ow + (size_t)o * L, L, on + o, acc)) rc = -1;
+    oe[o] = 0;
+  }
+  __gmpz_clear(acc); __gmpz_clear(y); __gmpz_clear(base); __gmpz_clear(t);
+  return rc;
+}
+
+/* chunking_cumsum_with_step in place: data[i+j] = add(data[i+j], data[i+j-step]), j ascending */
+int gref_cumsum(gref_ctx* c, int L, uint32_t* w, uint8_t* ng, int32_t* ex, long n, const int64_t* chunks,
+                long nchunks, long step) {
+  mpz_t a, b, t, e16;
+  __gmpz_init(a); __gmpz_init(b); __gmpz_init(t); __gmpz_init(e16);
+  int rc = 0;
+  long base = 0;
+  for (long ci = 0; ci < nchunks; ++ci) {
+    for (long j = step; j < chunks[ci]; ++j) {
+      const long d = base + j, s = d - step;
+      if (d >= n) { rc = -4; break; }
+      ld_ct(a, w + (size_t)d * L, L, ng[d]);
+      ld_ct(b, w + (size_t)s * L, L, ng[s]);
+      int ea = ex[d];
+      if (!is_literal_one(a) && is_literal_one(b)) continue;
+      fp_add_into(c, a, &ea, b, ex[s], t, e16);
+      if (st_ct(w + (size_t)d * L, L, ng + d, a)) rc = -1;
+      ex[d] = ea;
+    }
+    base += chunks[ci];
+  }
+  __gmpz_clear(a); __gmpz_clear(b); __gmpz_clear(t); __gmpz_clear(e16);
+  return rc;
+}
+
 /* ---------------- timed CPU baseline (same call sequence, per element) ---------------- */
 typedef struct {
   gref_ctx* c;

@@ -10,6 +10,8 @@ import os
 import subprocess
 from typing import Optional
 
+import numpy as np
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "build", "libgmpref.so")
 _lib = None
@@ -37,6 +39,11 @@ def load():
                                     ctypes.c_size_t]
         lib.gref_powm.argtypes = [ctypes.c_char_p] * 4 + [ctypes.c_size_t]
         lib.gref_tdiv_r.argtypes = [ctypes.c_char_p] * 3 + [ctypes.c_size_t]
+        P, L_, I = ctypes.c_void_p, ctypes.c_long, ctypes.c_int
+        lib.gref_fold.argtypes = [P, I, P, P, P, P, P, L_, P, P, P, L_, I]
+        lib.gref_mul.argtypes = [P, I, P, P, P, I, P, P, P, L_, P, P, P, I]
+        lib.gref_squeeze.argtypes = [P, I, P, P, L_, I, ctypes.c_ulong, P, P, P]
+        lib.gref_cumsum.argtypes = [P, I, P, P, P, L_, P, L_, L_]
         lib.gref_bench.restype = ctypes.c_double
         lib.gref_bench.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_ulong]
         _lib = lib
@@ -80,11 +87,102 @@ class GmpKey:
         load().gref_add_ct(self.ctx, _h(a), _h(b), out, self.cap)
         return _int(out)
 
+    # ---- bulk vector checkers: numpy (words [count, L] uint32, neg [count] uint8,
+    # exp [count] int32) -- the reference's signed integers, as fphe_export_signed writes them
+    def fold(self, src, terms, slots, acc, threads: int = 0):
+        """acc[slots[k]] = Ciphertext::add(acc[slots[k]], src[terms[k]]) for k ascending (the
+        reference's iupdate / intervals_sum / matmul loops).  src and acc are (words, neg, exp)
+        triples; returns the new acc triple."""
+        sw, sn, se = _vec(src)
+        aw, an, ae = (x.copy() for x in _vec(acc))
+        t = np.ascontiguousarray(terms, dtype=np.int64)
+        s_ = np.ascontiguousarray(slots, dtype=np.int64)
+        if t.shape != s_.shape or (t.size and (t.min() < 0 or t.max() >= len(sn) or s_.min() < 0
+                                               or s_.max() >= len(an))):
+            raise ValueError("gref_fold: bad term/slot indexes")
+        rc = load().gref_fold(self.ctx, sw.shape[1], _p(sw), _p(sn), _p(se), _p(t), _p(s_), t.size, _p(aw), _p(an),
+                              _p(ae), len(an), _threads(threads))
+        if rc:
+            raise RuntimeError(f"gref_fold rc={rc}")
+        return aw, an, ae
+
+    def mul(self, src, pt, threads: int = 0):
+        """Ciphertext::mul element-wise; pt = (signed significand words [count, Lp], neg, exp)."""
+        sw, sn, se = _vec(src)
+        pw, pn, pe = _vec(pt)
+        n = len(sn)
+        ow, on, oe = np.zeros_like(sw), np.zeros(n, np.uint8), np.zeros(n, np.int32)
+        rc = load().gref_mul(self.ctx, sw.shape[1], _p(sw), _p(sn), _p(se), pw.shape[1], _p(pw), _p(pn), _p(pe), n,
+                             _p(ow), _p(on), _p(oe), _threads(threads))
+        if rc:
+            raise RuntimeError(f"gref_mul rc={rc}")
+        return ow, on, oe
+
+    def squeeze(self, src, pack_num: int, shift_bit: int):
+        sw, sn, _ = _vec(src)
+        n = len(sn)
+        m = -(-n // pack_num)
+        ow, on, oe = np.zeros((m, sw.shape[1]), np.uint32), np.zeros(m, np.uint8), np.zeros(m, np.int32)
+        rc = load().gref_squeeze(self.ctx, sw.shape[1], _p(sw), _p(sn), n, pack_num, shift_bit, _p(ow), _p(on), _p(oe))
+        if rc:
+            raise RuntimeError(f"gref_squeeze rc={rc}")
+        return ow, on, oe
+
+    def cumsum(self, vec, chunk_sizes, step: int):
+        w, ng, ex = (x.copy() for x in _vec(vec))
+        ch = np.ascontiguousarray(chunk_sizes, dtype=np.int64)
+        rc = load().gref_cumsum(self.ctx, w.shape[1], _p(w), _p(ng), _p(ex), len(ng), _p(ch), ch.size, step)
+        if rc:
+            raise RuntimeError(f"gref_cumsum rc={rc}")
+        return w, ng, ex
+
     def bench(self, op: str, per_thread: int, threads: int = 1, seed: int = 1) -> float:
         """Wall seconds for threads x per_thread elements of op in {'encrypt', 'decrypt', 'add',
         'add_gap'} ('add_gap': ct-add with the Hetero-LR exponent-gap mix, see gmp_ref.c)."""
         code = {"encrypt": 0, "decrypt": 1, "add": 2, "add_gap": 3, "mul": 4, "iupdate": 5}[op]
         return load().gref_bench(self.ctx, code, per_thread, threads, seed)
+
+
+def _vec(v):
+    w, ng, ex = v
+    return (np.ascontiguousarray(w, dtype=np.uint32), np.ascontiguousarray(ng, dtype=np.uint8),
+            np.ascontiguousarray(ex, dtype=np.int32))
+
+
+def _p(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def _threads(k: int) -> int:
+    """Worker threads: k, else the CPUs this process may use (the GPU box's cgroup quota is 16
+    of a many-core host), at most 16."""
+    if k > 0:
+        return k
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return max(1, min(16, int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+def to_vec(cs, exps, L: int):
+    """Python signed ints + exps -> the (words, neg, exp) triple."""
+    w = np.zeros((len(cs), L), np.uint32)
+    for i, c in enumerate(cs):
+        m = abs(int(c))
+        w[i] = np.frombuffer(m.to_bytes(4 * L, "little"), dtype=np.uint32)
+    return w, np.array([1 if c < 0 else 0 for c in cs], np.uint8), np.array(list(exps), np.int32)
+
+
+def from_vec(v):
+    """(words, neg, exp) -> (Python signed ints, exps)."""
+    w, ng, ex = _vec(v)
+    nb = 4 * w.shape[1]
+    raw = w.tobytes()
+    mags = [int.from_bytes(raw[i * nb:(i + 1) * nb], "little") for i in range(w.shape[0])]
+    return [-m if s else m for m, s in zip(mags, ng.tolist())], ex.tolist()
 
 
 def powm(b: int, e: int, m: int) -> int:

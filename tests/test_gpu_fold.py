@@ -16,6 +16,10 @@ from oracle import paillier_oracle as O
 
 from test_gpu_ops import dev_vec, host, load, more  # noqa: E402
 
+import numpy as np  # noqa: E402
+
+from oracle import gmp_ref  # noqa: E402
+
 pytestmark = pytest.mark.gpu
 
 
@@ -29,6 +33,23 @@ def oracle_fold(opk, src, idx, seg, nseg):
     for i, s in zip(idx, seg):
         out[s] = O.ct_add(opk, out[s], src[i])
     return [(c.c, c.exp) for c in out]
+
+
+def gmp_spot_check(pk, src, idx, seg, got, segs):
+    """libgmp's sequential fold (oracle/gmp_ref.c gref_fold: the reference's add_assign loop,
+    term order kept) of the segments `segs`, against the device's result `got` (host pairs):
+    the large folds' slot plans are pinned to libgmp, not only to another device mode."""
+    L = pk._key.L2
+    segs = sorted(segs)
+    sv = gmp_ref.to_vec([c.c for c in src], [c.exp for c in src], L)
+    idx_np = np.asarray(idx.cpu() if isinstance(idx, torch.Tensor) else idx, dtype=np.int64)
+    seg_np = np.asarray(seg.cpu() if isinstance(seg, torch.Tensor) else seg, dtype=np.int64)
+    keep = np.isin(seg_np, segs)
+    slots = np.searchsorted(np.array(segs), seg_np[keep])
+    want = gmp_ref.from_vec(gmp_ref.GmpKey(pk.n).fold(sv, idx_np[keep], slots,
+                                                       gmp_ref.to_vec([1] * len(segs), [0] * len(segs), L),
+                                                       threads=len(segs)))
+    assert [got[s] for s in segs] == list(zip(*want))
 
 
 def mixed_sources(opk, cts, k, seed):
@@ -236,6 +257,9 @@ def test_fold_raised_keys_auto_matches_merge(bits, monkeypatch):
     monkeypatch.setenv("FPHE_FOLD_RAISE", "0")
     want = host(pk, P._fold_to_segments(pk, v, seg, 64, index=idx))
     assert got == want
+    # and against libgmp: six segments of ~33k terms, each with outliers below its bulk (every
+    # later term pays decrese_exp_to's powm there: ~0.4 ms per term on one core)
+    gmp_spot_check(pk, src, idx, seg, got, [0, 9, 22, 40, 51, 63])
 
 
 def test_fold_raised_keys_past_the_cap(env, monkeypatch):
@@ -280,5 +304,10 @@ def test_fold_raised_keys_multi_round_plan(monkeypatch):
             monkeypatch.setenv("FPHE_FOLD_RAISE", mode)
         r = P._fold_to_segments(pk, v, seg, 500, index=idx)
         outs.append((r.C[: (500 + 63) // 64].clone(), r.sign[:500].clone(), r.exp[:500].clone()))
+        if mode is None:
+            auto = host(pk, r)
     for o in outs[1:]:
         assert all(torch.equal(a, b) for a, b in zip(outs[0], o))
+    # two segments of ~72k terms against libgmp (~30 s: most terms need an exponent alignment)
+    src = [O.Ciphertext(c.c, e) for c, e in zip(base, exps)]
+    gmp_spot_check(pk, src, idx, seg, auto, [7, 311])

@@ -145,3 +145,21 @@ def test_iupdate_exact_gap_between_histogram_and_terms(k1024):
     want = [O.Ciphertext(c, e) for c, e in zip(hc, hexps)]
     O.iupdate(opk, want, [O.Ciphertext(c, e) for c, e in zip(cs, exps)], positions, 1)
     assert hist.to_signed_ints(pk.ns) == ([w.c for w in want], [w.exp for w in want])
+
+
+def test_forced_raise_skips_gap_beyond_kernel_limit(k1024, monkeypatch):
+    """FPHE_FOLD_RAISE=force makes every key above its segment's least exponent a raise
+    candidate; a key 65,537 steps up is beyond what k_segfold27 squares (4 kMaxGap) and must
+    stay out of the slot plan: the fold then takes the exact path and matches the
+    reference's sequential iupdate.  The segment also holds a key 2 steps up, which is raised."""
+    sk, pk, coder, osk, opk, _ = k1024
+    cs = _cts(opk, 6, 13)
+    exps = [-65537, 0, -65535, -65535, -65537, 1]
+    monkeypatch.setenv("FPHE_FOLD_RAISE", "force")
+    src = _unpickled(pk, cs, exps)
+    hist = P.CiphertextVector.zeros(2, pk._key.L2)
+    positions = [[0], [0], [0, 1], [0], [1], [1]]
+    hist.iupdate(src, positions, 1, pk)
+    want = [O.ct_zero() for _ in range(2)]
+    O.iupdate(opk, want, [O.Ciphertext(c, e) for c, e in zip(cs, exps)], positions, 1)
+    assert hist.to_signed_ints(pk.ns) == ([w.c for w in want], [w.exp for w in want])

@@ -241,3 +241,71 @@ def test_fixtures_reproducible():
         assert hex(pt.significant) == e["sig"][i] and pt.exp == e["exp"][i]
         c = O.fp_encrypt(pk, pt, True, int(e["r"][i], 16))
         assert hex(c.c) == e["ct"][i]
+
+
+# ---- the bulk libgmp checkers (oracle/gmp_ref.c gref_fold / gref_mul / gref_squeeze /
+# gref_cumsum) that the large -m gpu parity tests use, pinned against the Python restatement
+def _signed_sources(pk, k, seed):
+    """k signed ciphertext integers with spread exponents and literal 1s (the fold's traps)."""
+    rng = random.Random(seed)
+    out = []
+    for _ in range(k):
+        r = rng.random()
+        if r < 0.08:
+            out.append(O.Ciphertext(1, rng.choice([0, -14, -3])))
+        else:
+            c = rng.randrange(1, pk.ns)
+            out.append(O.Ciphertext(-c if rng.random() < 0.4 else c, rng.choice([-16, -14, -13, -13, -12, -9, 2])))
+    return out
+
+
+@pytest.mark.parametrize("bits", [1024, 2048])
+def test_bulk_fold_matches_oracle(gmp, bits):
+    fx, sk, pk = keys(bits)
+    g = gmp.GmpKey(pk.n)
+    L = pk.ns.bit_length() // 32 + 1
+    src = _signed_sources(pk, 90, bits)
+    rng = random.Random(bits + 1)
+    nslots = 13
+    acc = [O.ct_zero() for _ in range(nslots)]
+    acc[3] = src[5]  # a slot that starts from a real ciphertext
+    terms = [rng.randrange(len(src)) for _ in range(600)]
+    slots = [rng.randrange(nslots - 2) for _ in range(600)]  # two slots see no term
+    want = list(acc)
+    for t, s in zip(terms, slots):
+        want[s] = O.ct_add(pk, want[s], src[t])
+    sv = gmp.to_vec([c.c for c in src], [c.exp for c in src], L)
+    av = gmp.to_vec([c.c for c in acc], [c.exp for c in acc], L)
+    for threads in (1, 3):
+        got = gmp.from_vec(g.fold(sv, terms, slots, av, threads=threads))
+        assert got == ([c.c for c in want], [c.exp for c in want])
+
+
+@pytest.mark.parametrize("bits", [1024, 2048])
+def test_bulk_mul_squeeze_cumsum_match_oracle(gmp, bits):
+    fx, sk, pk = keys(bits)
+    g = gmp.GmpKey(pk.n)
+    L = pk.ns.bit_length() // 32 + 1
+    src = [c for c in _signed_sources(pk, 40, bits + 7)]
+    rng = random.Random(bits + 3)
+    # ct x pt: float significands of both signs, encoded negative ints (the invert branch)
+    pts = []
+    for i in range(len(src)):
+        if i % 4 == 3:
+            pts.append(O.encode_i64(pk.n, -rng.randrange(1, 1 << 40)))
+        else:
+            pts.append(O.encode_f32(pk.n, float(np.float32(rng.uniform(-2, 2)))))
+    want = [O.ct_mul(pk, c, p) for c, p in zip(src, pts)]
+    Lp = max(1, max(abs(p.significant).bit_length() for p in pts) // 32 + 1)
+    pv = gmp.to_vec([p.significant for p in pts], [p.exp for p in pts], Lp)
+    got = gmp.from_vec(g.mul(gmp.to_vec([c.c for c in src], [c.exp for c in src], L), pv, threads=2))
+    assert got == ([c.c for c in want], [c.exp for c in want])
+    # pack_squeeze over a ragged last chunk
+    want = O.pack_squeeze(pk, src[:23], 3, 140)
+    got = gmp.from_vec(g.squeeze(gmp.to_vec([c.c for c in src[:23]], [c.exp for c in src[:23]], L), 3, 140))
+    assert got == ([c.c for c in want], [c.exp for c in want])
+    # chunking_cumsum_with_step
+    data = list(src[:30])
+    O.chunking_cumsum_with_step(pk, data, [8, 12, 10], 2)
+    got = gmp.from_vec(g.cumsum(gmp.to_vec([c.c for c in src[:30]], [c.exp for c in src[:30]], L), [8, 12, 10], 2))
+    assert got == ([c.c for c in data], [c.exp for c in data])
