@@ -249,15 +249,16 @@ def valu_roofline(kernel: str, mac32: float, ms: float, hbm_bytes: float, traffi
 
 
 class ClockMeter:
-    """The shader clock a timed leg ran at: fphe_clock_stamp queues one-wave
-    workgroups on the leg's stream just before and just after it; each writes its XCD's
-    shader-clock cycle counter and the constant-rate counter, so (cycles1 - cycles0) /
-    (wall1 - wall0) per XCD is that XCD's mean clock over the leg.  The rooflines price at
-    2.4 GHz; `frac_at_measured_clock` = frac x 2.4 / measured GHz separates a slow box's clock
-    from the code."""
+    """The shader clock a timed leg ran at: fphe_clock_stamp queues 2048
+    one-wave workgroups on the leg's stream just before and just after it (~10 us each); each
+    writes its CU's shader-clock cycle counter and the constant-rate counter, so (cycles1 -
+    cycles0) / (wall1 - wall0) per CU stamped on both sides is that CU's mean clock over the
+    leg (the counters of different CUs are not synchronised).  The rooflines price at 2.4 GHz;
+    `frac_at_measured_clock` = frac x 2.4 / measured GHz separates a slow box's clock from the
+    code."""
 
-    BLOCKS = 32
-    SLOTS = 256
+    BLOCKS = 2048
+    SLOTS = 64
 
     def __init__(self, dev, stream):
         import ctypes
@@ -278,22 +279,28 @@ class ClockMeter:
         return i
 
     def ghz(self, i0: int, i1: int):
-        """Mean shader clock (GHz) between two stamps, over the XCDs seen in both (call after a
-        synchronize); None when the counters give nothing usable."""
-        a = self.buf[i0].view(-1, 3).cpu().tolist()
-        b = self.buf[i1].view(-1, 3).cpu().tolist()
-        first = lambda rows: {int(x): (int(cy), int(w)) for x, cy, w in reversed(rows)}
+        """Median (and spread) over CUs of the mean shader clock (GHz) between two stamps (call
+        after a synchronize); None when no CU was stamped on both sides."""
+        a = self.buf[i0].view(-1, 3).cpu().numpy().astype(np.uint64)
+        b = self.buf[i1].view(-1, 3).cpu().numpy().astype(np.uint64)
+
+        def first(rows):
+            cu, idx = np.unique(rows[:, 0], return_index=True)
+            return dict(zip(cu.tolist(), idx.tolist()))
+
         fa, fb = first(a), first(b)
         per = []
-        for x in sorted(set(fa) & set(fb)):
-            dc = (fb[x][0] - fa[x][0]) & ((1 << 64) - 1)
-            dw = ((fb[x][1] - fa[x][1]) & ((1 << 64) - 1)) / (self.khz.value * 1e3)
-            if dw > 0:
+        for cu in set(fa) & set(fb):
+            ra, rb = a[fa[cu]], b[fb[cu]]
+            dc = int(rb[1]) - int(ra[1])
+            dw = (int(rb[2]) - int(ra[2])) / (self.khz.value * 1e3)
+            if dw > 0 and dc > 0:
                 per.append(dc / dw / 1e9)
         if not per or not self.khz.value:
             return None
-        return {"GHz": round(sum(per) / len(per), 4), "min": round(min(per), 4), "max": round(max(per), 4),
-                "xcds": len(per)}
+        per.sort()
+        return {"GHz": round(per[len(per) // 2], 4), "p10": round(per[len(per) // 10], 4),
+                "p90": round(per[(9 * len(per)) // 10], 4), "cus": len(per)}
 
 
 def at_clock(frac: float, clock) -> dict:

@@ -2317,23 +2317,25 @@ fphe_status fphe_wire_decode(const uint8_t* buf, const int64_t* dig_off, const i
 }
 
 // Shader-clock stamps (diagnostics; bench.py's per-leg clock).  `blocks`
-// one-wave workgroups, dealt round-robin over the XCDs by the dispatcher; lane 0 of block b
-// writes {XCC id, shader-clock counter (clock64: s_memtime, counts SCLK cycles), constant-rate
-// counter (wall_clock64)} to out[3b .. 3b+2] with vector stores.  Two stamps queued on the
-// stream around a launch give each XCD's mean shader clock over it (the counters of different
-// XCDs are not synchronised, so the host pairs stamps by XCC id).
+// one-wave workgroups; lane 0 of block b writes {its CU's place -- XCC id << 16 | the SE, SH
+// and CU fields of HW_ID --, the shader-clock counter (clock64: s_memtime, counts SCLK
+// cycles), the constant-rate counter (wall_clock64)} to out[3b .. 3b+2] with vector stores.
+// The shader-clock counters of different CUs are not synchronised (a before/after pair from
+// two CUs of one XCD can even run backwards), so the host pairs two stamps queued around a
+// launch by CU; with a few thousand blocks every CU is stamped on both sides.
 __global__ __launch_bounds__(64) void k_clock_stamp(unsigned long long* __restrict__ out) {
   if (threadIdx.x != 0) return;
   const unsigned long long c = clock64();
   const unsigned long long w = wall_clock64();
-  const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 15u;  // HW_REG_XCC_ID
-  out[3 * blockIdx.x] = xcc;
+  const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 15u;   // HW_REG_XCC_ID
+  const unsigned hw = __builtin_amdgcn_s_getreg((7 << 11) | (8 << 6) | 4) & 255u;    // HW_ID[15:8]
+  out[3 * blockIdx.x] = (xcc << 16) | hw;
   out[3 * blockIdx.x + 1] = c;
   out[3 * blockIdx.x + 2] = w;
 }
 
 fphe_status fphe_clock_stamp(uint64_t* out, uint32_t blocks, uint32_t* wall_khz, void* stream) {
-  if (!out || blocks == 0 || blocks > 1024) return FPHE_ERR_ARG;
+  if (!out || blocks == 0 || blocks > 65536) return FPHE_ERR_ARG;
   if (wall_khz) {
     int dev = 0, khz = 0;
     if (hipGetDevice(&dev) != hipSuccess ||

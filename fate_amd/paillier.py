@@ -481,6 +481,7 @@ class PlaintextVector:
         from . import wire
         v = wire.plaintext_vector_from_bincode(bytes(state))
         self.P, self.neg, self.exp, self.count = v.P, v.neg, v.exp, v.count
+        self.ebound = v.ebound
 
 
 class Plaintext:
@@ -637,6 +638,7 @@ class CiphertextVector:
             raise ValueError("bincode CiphertextVector: trailing bytes")
         self.C, self.sign, self.exp, self.count, self.n, self.raw = v.C, v.sign, v.exp, v.count, v.n, v.raw
         self.lit = False
+        self.ebound = None  # crafted or foreign exponents: every add checks its gaps
 
     def __copy__(self) -> "CiphertextVector":
         """A device-side clone (the key and raw state travel; no wire round trip)."""

@@ -329,11 +329,12 @@ fphe_status fphe_chacha20_blocks(const uint32_t key[8], uint32_t counter, const 
                                  uint32_t* out, void* stream);
 
 /* Diagnostics: shader-clock stamps (not part of the reference's surface; bench.py reports the
- * clock each timed leg ran at).  Queues `blocks` (1..1024) one-wave workgroups on `stream`;
- * block b writes out[3b] = its XCC (XCD) id, out[3b+1] = the shader-clock cycle counter,
- * out[3b+2] = the constant-rate counter, whose rate in kHz goes to *wall_khz when non-NULL.
- * out is a DEVICE buffer of 3*blocks uint64.  (c1 - c0) / (w1 - w0) * wall_khz * 1e3 over two
- * stamps of the same XCD is that XCD's mean clock between them. */
+ * clock each timed leg ran at).  Queues `blocks` (1..65536) one-wave workgroups on `stream`;
+ * block b writes out[3b] = the CU it ran on (XCC id << 16 | HW_ID bits 15:8: CU, SH, SE),
+ * out[3b+1] = that CU's shader-clock cycle counter, out[3b+2] = the constant-rate counter,
+ * whose rate in kHz goes to *wall_khz when non-NULL.  out is a DEVICE buffer of 3*blocks
+ * uint64.  (c1 - c0) / (w1 - w0) * wall_khz * 1e3 over two stamps of the same CU is its mean
+ * clock between them (the cycle counters of different CUs are not synchronised). */
 fphe_status fphe_clock_stamp(uint64_t* out, uint32_t blocks, uint32_t* wall_khz, void* stream);
 
 #ifdef __cplusplus
