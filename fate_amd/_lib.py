@@ -38,7 +38,7 @@ EXPORTED_SYMBOLS = (
     "fphe_encrypt", "fphe_encrypt_crt", "fphe_decrypt", "fphe_add", "fphe_add_ordered", "fphe_add_order", "fphe_mul", "fphe_neg", "fphe_sqmul", "fphe_align",
     "fphe_fold", "fphe_fold_segments", "fphe_permute", "fphe_export_signed", "fphe_import_signed",
     "fphe_wire_lengths", "fphe_wire_encode", "fphe_wire_scan", "fphe_wire_decode", "fphe_chacha20_blocks",
-    "fphe_clock_stamp",
+    "fphe_clock_stamp", "fphe_pack_squeeze",
 )
 
 _lock = threading.Lock()
@@ -133,6 +133,8 @@ def load() -> ctypes.CDLL:
         lib.fphe_chacha20_blocks.restype = st
         lib.fphe_clock_stamp.argtypes = [vp, ctypes.c_uint32, vp, vp]
         lib.fphe_clock_stamp.restype = st
+        lib.fphe_pack_squeeze.argtypes = [vp, vp, vp, sz, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp]
+        lib.fphe_pack_squeeze.restype = st
         lib.fphe_wire_lengths.argtypes = [vp, vp, ctypes.c_uint32, sz, vp, vp, vp]
         lib.fphe_wire_encode.argtypes = [vp, vp, vp, ctypes.c_uint32, sz, vp, vp, vp, vp, vp]
         lib.fphe_wire_scan.argtypes = [vp, sz, sz, sz, vp, vp, vp, vp, vp, vp]

@@ -514,6 +514,7 @@ __global__ __launch_bounds__(256) void k_decode_f64(KeyArgs K, const u32* __rest
 #include "kernels27.h"
 namespace {
 #include "group_dev.h"
+#include "wide_dev.h"
 }  // namespace
 
 // ======================================================================================
@@ -2138,6 +2139,30 @@ fphe_status fphe_sqmul(fphe_ctx* c, const uint32_t* Ca, const uint32_t* Cb, cons
   return launch_sqmul27<64>(c, Ca, Cb, sb, (int)nsq, count, Co, so, (hipStream_t)stream);
 }
 
+
+// pack_squeeze with one chunk per wave (wide_dev.h): for few chunks, where the throughput
+// engine would run each squaring step as a launch of nearly empty waves
+fphe_status fphe_pack_squeeze(fphe_ctx* c, const uint32_t* C, const uint8_t* sign, size_t count, uint32_t pack_num,
+                              uint32_t shift_bit, uint32_t* Co, uint8_t* so, void* stream) {
+  if (!c) return FPHE_ERR_ARG;
+  if (count == 0) return FPHE_OK;
+  if (!C || !sign || !Co || !so || pack_num == 0 || shift_bit > (1u << 20)) return FPHE_ERR_ARG;
+  const size_t nch = (count + pack_num - 1) / pack_num;
+  if (nch > (size_t)1 << 31) return FPHE_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DevGuard g(c->device);
+  hipStream_t s = (hipStream_t)stream;
+  if (c->L2 == 256)
+    hipLaunchKernelGGL(k_squeeze_wide<256>, dim3((unsigned)nch), dim3(64), 0, s, c->K, C, sign, count, (int)pack_num,
+                       (int)shift_bit, Co, so);
+  else if (c->L2 == 128)
+    hipLaunchKernelGGL(k_squeeze_wide<128>, dim3((unsigned)nch), dim3(64), 0, s, c->K, C, sign, count, (int)pack_num,
+                       (int)shift_bit, Co, so);
+  else
+    hipLaunchKernelGGL(k_squeeze_wide<64>, dim3((unsigned)nch), dim3(64), 0, s, c->K, C, sign, count, (int)pack_num,
+                       (int)shift_bit, Co, so);
+  return hip_ok(hipGetLastError());
+}
 
 fphe_status fphe_align(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, const int32_t* gap, size_t count,
                        uint32_t* Co, uint8_t* so, void* stream) {

@@ -990,6 +990,18 @@ class CiphertextVector:
         """``CiphertextVector::pack_squeeze`` (paillier.rs:241; lib.rs:439-450): per chunk of
         pack_num, acc = x0; acc = acc^(2^offset_bit) * y mod n^2 for each further y; exp 0."""
         n = self.count
+        nch = -(-n // pack_num) if pack_num > 0 else 0
+        if 0 < nch <= WIDE_SQUEEZE_MAX_CHUNKS and pack_num > 1:
+            # few chunks: the whole squeeze in one launch, one chunk per wave (fphe_pack_squeeze)
+            dev = self.device
+            src = _fit_limbs(self, pk._key.L2)
+            out = CiphertextVector.empty(nch, pk._key.L2, dev)
+            _lib.check(_lib.load().fphe_pack_squeeze(pk._key.ctx(dev), _ptr(src.C), _ptr(src.sign), n, pack_num,
+                                                     int(offset_bit), _ptr(out.C), _ptr(out.sign),
+                                                     ctypes.c_void_p(_stream(dev))), "fphe_pack_squeeze")
+            out.n = pk.n
+            out.ebound = (0, 0)
+            return out
         heads = torch.arange(0, n, pack_num)
         acc = self._gather(heads)
         for j in range(1, pack_num):
@@ -1220,6 +1232,9 @@ def _flatten_positions(indexes, dev=None) -> Tuple[torch.Tensor, torch.Tensor]:
     return ii.to(dev), pp.to(dev)
 
 
+# pack_squeeze takes the one-chunk-per-wave kernel (fphe_pack_squeeze) up to this many chunks:
+# beyond it the throughput kernel's full waves issue the squarings more cheaply
+WIDE_SQUEEZE_MAX_CHUNKS = int(os.environ.get("FPHE_WIDE_SQUEEZE_MAX", "4096"))
 ADD_REGIONS = 8  # kAddRegions in fate_phe.hip: runs of k_add27 wave tiles, one per XCD
 # FPHE_ADD_REGION_SORT=0: one global gap sort (round-2 order; same-box A/B in tools/)
 _ADD_REGION_SORT = os.environ.get("FPHE_ADD_REGION_SORT", "1") != "0"

@@ -252,6 +252,16 @@ fphe_status fphe_fold_segments(fphe_ctx* ctx, const uint32_t* Src, const uint8_t
 fphe_status fphe_sqmul(fphe_ctx* ctx, const uint32_t* Ca, const uint32_t* Cb, const uint8_t* sb, uint32_t nsq,
                        size_t count, uint32_t* Co, uint8_t* so, void* stream);
 
+/* The whole CiphertextVector::pack_squeeze (paillier.rs:241-243; fixedpoint_paillier/src/lib.rs:
+ * 439-450) in one launch: for each chunk c of pack_num elements of C (the last may be short),
+ * acc = x_0, then acc = acc^(2^shift_bit) * y (tdiv n^2) for each further y; Co[c] = acc and
+ * so[c] = the sign the reference's integer has (x_0's for a one-element chunk, else the last
+ * y's).  One chunk per wave (a latency kernel, wide_dev.h): for calls with few chunks, where
+ * fphe_sqmul would run each step as a launch of nearly empty waves.  Co holds
+ * ceil(count / pack_num) elements; the caller sets their exponents to 0. */
+fphe_status fphe_pack_squeeze(fphe_ctx* ctx, const uint32_t* C, const uint8_t* sign, size_t count, uint32_t pack_num,
+                              uint32_t shift_bit, uint32_t* Co, uint8_t* so, void* stream);
+
 /* Co = Ca^(16^gap[i]) mod n^2 per element (gap >= 0), so = 0 where gap > 0 (canonical powm),
  * sa where gap == 0 (copied through): the exponent-alignment step of Ciphertext::add,
  * decrese_exp_to (fixedpoint_paillier/src/lib.rs:250-258), for many elements at once.  The

@@ -326,6 +326,10 @@ def test_other_key_sizes_bit_exact(bits):
     dec = sk.decrypt_to_encoded(s).to_ints()
     od = [O.fp_decrypt(osk, t) for t in O.vec_add(opk, oc, oy)]
     assert dec == ([d.significant for d in od], [d.exp for d in od])
+    # pack_squeeze on the one-chunk-per-wave kernel at this geometry (wide_dev.h)
+    sq = c.pack_squeeze(3, 61, pk)
+    osq = O.pack_squeeze(opk, oc, 3, 61)
+    assert sq.to_signed_ints(pk.ns) == ([t.c for t in osq], [t.exp for t in osq])
 
 
 def test_unsupported_key_sizes_decline():

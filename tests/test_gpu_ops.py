@@ -176,6 +176,20 @@ def test_pack_squeeze(env):
         assert host(pk, got) == ref(O.pack_squeeze(opk, data, pack_num, shift))
 
 
+@pytest.mark.parametrize("wide_max", [4096, 0])
+def test_pack_squeeze_wide_and_stepwise(env, monkeypatch, wide_max):
+    """pack_squeeze (lib.rs:439-450) on both device paths -- fphe_pack_squeeze, one chunk per
+    wave (wide_dev.h: WIDE_SQUEEZE_MAX_CHUNKS = 4096), and the fphe_sqmul step launches (0) --
+    on negative signed ciphertexts (the result takes the last multiplied y's sign, or x_0's in
+    a one-element chunk), config 4's 13-way squeeze at 148 bits, shift 0 and 1."""
+    monkeypatch.setattr(P, "WIDE_SQUEEZE_MAX_CHUNKS", wide_max)
+    fx, sk, pk, coder, opk, cts = env
+    data = more(opk, cts, 61, 7)
+    for pack_num, shift in ((13, 148), (4, 1), (2, 0), (5, 37)):
+        got = dev_vec(pk, data).pack_squeeze(pack_num, shift, pk)
+        assert host(pk, got) == ref(O.pack_squeeze(opk, data, pack_num, shift)), (pack_num, shift)
+
+
 def test_iupdate_and_masks(env):
     fx, sk, pk, coder, opk, cts = env
     rng = random.Random(7)
