@@ -7,11 +7,12 @@
 // nearly empty wave per chain at that wave's per-row latency (~22 us per 4096-bit squaring).
 // Here one element spans a whole wave: lane l < NLANE holds the K = TPI limbs [K l, K l + K)
 // (the same 28-bit limbs and the same R = 2^(LB NL) as the throughput engine, so M-form
-// vectors need no conversion), a row is K operand + K reduction MACs per lane, m comes from
-// lane 0 by v_readfirstlane, and the reduction word crosses lanes by DPP row_shl:1 with the
-// three 16-lane row boundaries patched by v_readlane / v_writelane.  A row is ~20 instructions
-// instead of ~64, so a chain runs several times faster; per element it issues ~2.3x the MACs
-// of the throughput engine, so the launchers use it only when a call has few chains.
+// vectors need no conversion), a row is K operand + K reduction MACs per lane, the row's
+// multiplier comes from its lane by v_readlane, m from lane 0 by v_readfirstlane and two SALU
+// ops, and the reduction word crosses lanes by one wavefront-wide DPP shift.  A row is ~16
+// instructions instead of ~72, so a chain runs several times faster; per element it issues
+// ~2.3x the MACs of the throughput engine, so the launchers use it only when a call has few
+// chains.
 //
 // Lanes NLANE..63 hold zero limbs (A = N = 0) and stay zero: their T never receives anything
 // (the top lane keeps its carry, below), so no lane masks are needed in the rows.
@@ -29,12 +30,10 @@ struct Geo {
   static constexpr u32 MASK = (1u << LB) - 1u;
   // LDS words an element's number is read through: every limb's two words exist (zeros past L)
   static constexpr int WL = (NL * LB) / 32 + 3;
-  // a slot takes <= 2 products < 2^(2 LB + 0.01) per row (operand, reduction); the carry
-  // sweeps cut the rows into PARTS so a 64-bit slot never overflows
-  static constexpr int PARTS = (2 * NL + 4 <= (1 << (64 - 2 * LB))) ? 1
-                               : ((NL + 4 <= (1 << (64 - 2 * LB))) ? 2 : 4);
-  static_assert(2 * NL / PARTS + 4 <= (1 << (64 - 2 * LB)), "rows between sweeps overflow a slot");
-  static_assert(NL % PARTS == 0, "sweeps between whole rows");
+  // a slot takes <= 2 products < 2^(2 LB + 0.01) per row (operand, reduction): a carry sweep
+  // after every GP groups of K rows (the rows of one lane's limbs of B) keeps it in 64 bits
+  static constexpr int GP = ((1 << (64 - 2 * LB)) - 4) / 2 / K;
+  static_assert(GP >= 1 && 2 * K * GP + 4 <= (1 << (64 - 2 * LB)), "rows between sweeps overflow a slot");
   static_assert(NLANE <= 64, "one element per wave");
 };
 
@@ -49,36 +48,25 @@ __device__ __forceinline__ u64 wmads(u32 a, u32 b_uniform, u64 c) {  // b in an 
   return d;
 }
 
-// lane `to` of r takes lane `from` of x (v_readlane into an SGPR, then v_writelane)
-template <int from, int to>
-__device__ __forceinline__ int patch_lane(int r, int x) {
-  int t;
-  asm volatile("v_readlane_b32 %[t], %[x], %[f]\n\ts_nop 1\n\tv_writelane_b32 %[r], %[t], %[to]"
-               : [r] "+v"(r), [t] "=&s"(t)
-               : [x] "v"(x), [f] "i"(from), [to] "i"(to));
-  return r;
-}
-// lane i <- lane i + 1 (lane 63 <- 0): row_shl:1 inside the 16-lane rows, the row ends patched
+// lane i <- lane i + 1 (lane 63 <- 0) / lane i <- lane i - 1 (lane 0 <- 0): the GFX9
+// wavefront-wide DPP shifts wave_shl:1 / wave_shr:1, which gfx950 executes
+// (tools/probe/dpp_wave_probe.hip on MI355X, profiles/r05/r05e_dpp_wave_probe.txt): one
+// instruction where row_shl:1 needed a v_readlane / v_writelane patch per 16-lane row end
+template <int NLANE>
 __device__ __forceinline__ u32 from_next(u32 x) {
-  int r = __builtin_amdgcn_update_dpp(0, (int)x, 0x101, 0xf, 0xf, true);
-  r = patch_lane<16, 15>(r, (int)x);
-  r = patch_lane<32, 31>(r, (int)x);
-  r = patch_lane<48, 47>(r, (int)x);
-  return (u32)r;
+  return (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xf, 0xf, true);
 }
-// lane i <- lane i - 1 (lane 0 <- 0)
+template <int NLANE>
 __device__ __forceinline__ u32 from_prev(u32 x) {
-  int r = __builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);
-  r = patch_lane<15, 16>(r, (int)x);
-  r = patch_lane<31, 32>(r, (int)x);
-  r = patch_lane<47, 48>(r, (int)x);
-  return (u32)r;
+  return (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xf, 0xf, true);
 }
+template <int NLANE>
 __device__ __forceinline__ u64 from_prev64(u64 x) {
-  return ((u64)from_prev((u32)(x >> 32)) << 32) | from_prev((u32)x);
+  return ((u64)from_prev<NLANE>((u32)(x >> 32)) << 32) | from_prev<NLANE>((u32)x);
 }
 
-// CIOS row i of A * B: T += A b; m = T_0 n' mod 2^LB (lane 0's, broadcast through an SGPR);
+// CIOS row i of A * B: T += A b (b = B's limb i, wave-uniform in an SGPR); m = T_0 n' mod 2^LB
+// (lane 0's, broadcast through an SGPR);
 // T = (T + m N) / 2^LB with the positions shifted down one limb: a lane's bottom word X keeps
 // its high part (X >> LB stays at the new bottom) and hands X mod 2^LB to the lane below's top.
 template <int L>
@@ -86,14 +74,15 @@ __device__ __forceinline__ void row(u64 (&T)[Geo<L>::K], const u32 (&A)[Geo<L>::
                                     u32 np) {
   using G = Geo<L>;
   constexpr int K = G::K;
-  T[0] = wmad(A[0], b, T[0]);
-  const u32 m = __builtin_amdgcn_readfirstlane(((u32)T[0] * np) & G::MASK);
+  T[0] = wmads(A[0], b, T[0]);
+  // m on the scalar unit: lane 0's low word to an SGPR, then s_mul_i32 / s_and_b32
+  const u32 m = ((u32)__builtin_amdgcn_readfirstlane((int)(u32)T[0]) * np) & G::MASK;
 #pragma unroll
-  for (int k = 1; k < K; ++k) T[k] = wmad(A[k], b, T[k]);
+  for (int k = 1; k < K; ++k) T[k] = wmads(A[k], b, T[k]);
   const u64 X = wmads(N[0], m, T[0]);
 #pragma unroll
   for (int k = 1; k < K; ++k) T[k - 1] = wmads(N[k], m, T[k]);
-  const u32 up = from_next((u32)X & G::MASK);
+  const u32 up = from_next<G::NLANE>((u32)X & G::MASK);
   if constexpr (K > 1) {
     T[K - 1] = up;
     T[0] += X >> G::LB;
@@ -109,7 +98,7 @@ __device__ __forceinline__ void sweep(u64 (&T)[Geo<L>::K], int lane) {
   using G = Geo<L>;
   constexpr int K = G::K;
   const bool top = lane == G::NLANE - 1;
-  const u64 cin = from_prev64(top ? 0ull : (T[K - 1] >> G::LB));
+  const u64 cin = from_prev64<G::NLANE>(top ? 0ull : (T[K - 1] >> G::LB));
   const u64 keep_top = top ? ~0ull : (u64)G::MASK;
   if constexpr (K > 1) {
     T[K - 1] = (T[K - 1] & keep_top) + (T[K - 2] >> G::LB);
@@ -135,29 +124,26 @@ __device__ __forceinline__ void normalize(const u64 (&T)[Geo<L>::K], u32 (&A)[Ge
     A[j] = (u32)v & G::MASK;
     c = v >> G::LB;
   }
-  const u64 v = (u64)A[0] + from_prev64(c);
+  const u64 v = (u64)A[0] + from_prev64<G::NLANE>(c);
   A[0] = (u32)v & G::MASK;
   A[1] += (u32)(v >> G::LB);
 }
 
-// A <- A * B * R^-1 mod N, B's NL limbs in LDS (bl[i] = limb i, wave-uniform reads)
+// A <- A * B * R^-1 mod N (B may be A itself: A is rewritten only at the end).  Row i's
+// multiplier b_i = B's limb i is read from lane i / K with v_readlane (rows unrolled by K)
 template <int L>
-__device__ __forceinline__ void mul(u32 (&A)[Geo<L>::K], const u32* bl, const u32 (&N)[Geo<L>::K], u32 np, int lane) {
+__device__ __forceinline__ void mul(u32 (&A)[Geo<L>::K], const u32 (&B)[Geo<L>::K], const u32 (&N)[Geo<L>::K], u32 np,
+                                    int lane) {
   using G = Geo<L>;
-  constexpr int K = G::K, NL = G::NL, P = G::PARTS;
+  constexpr int K = G::K;
   u64 T[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) T[k] = 0;
-  u32 b = bl[0];
+#pragma unroll 1
+  for (int l = 0; l < G::NLANE; ++l) {
+    if (l && l % G::GP == 0) sweep<L>(T, lane);  // wave-uniform
 #pragma unroll
-  for (int part = 0; part < P; ++part) {
-    if (part) sweep<L>(T, lane);
-#pragma unroll 2
-    for (int i = part * (NL / P); i < (part + 1) * (NL / P); ++i) {
-      const u32 bn = bl[i + 1 < NL ? i + 1 : 0];  // the next row's multiplier, read ahead
-      row<L>(T, A, b, N, np);
-      b = bn;
-    }
+    for (int k = 0; k < K; ++k) row<L>(T, A, (u32)__builtin_amdgcn_readlane((int)B[k], l), N, np);
   }
   normalize<L>(T, A);
 }
@@ -256,14 +242,10 @@ __global__ __launch_bounds__(64) void k_squeeze_wide(KeyArgs K, const u32* __res
   wide::load_elem<L>(C, h, wl, A, lane);
   u8 sg = sign[h];
   for (int k = 1; k < len; ++k) {
-    for (int t = 0; t < shift; ++t) {  // acc^(2^shift): products of acc with itself
-      wide::to_lds<L>(A, bl, lane);
-      wide::mul<L>(A, bl, N, np, lane);
-    }
+    for (int t = 0; t < shift; ++t) wide::mul<L>(A, A, N, np, lane);  // acc^(2^shift)
     u32 B[G::K];
     wide::load_elem<L>(C, h + k, wl, B, lane);
-    wide::to_lds<L>(B, bl, lane);
-    wide::mul<L>(A, bl, N, np, lane);
+    wide::mul<L>(A, B, N, np, lane);
     sg = sign[h + k];
   }
   wide::store_elem<L>(A, bl, K.N2_27, Co, chunk, lane);
