@@ -25,6 +25,17 @@ namespace {
 
 constexpr int kBlock = 256;      // 4 waves per workgroup
 constexpr int kWavesPerBlock = kBlock / FPHE_WAVE;
+// decryptions of at most this many elements run their half-size modexps on the one-element-
+// per-wave latency kernel (wide_dev.h k_pow_half_wide): below ~1 wave per SIMD of the
+// throughput kernel every wave of it runs alone at its per-row latency
+// (env FPHE_WIDE_DECRYPT_MAX overrides, read once: 0 turns the path off, for A/B and tests)
+inline size_t wide_decrypt_max() {
+  static const size_t v = [] {
+    const char* e = getenv("FPHE_WIDE_DECRYPT_MAX");
+    return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)2048;
+  }();
+  return v;
+}
 constexpr int kWinSlide = 6;     // sliding window of the 27-bit engine's shared-exponent modexps
 // the decrypt halves of <= 1024-bit keys (TPI 1, exponents p-1 / q-1 of <= 512 bits): a 5-bit
 // window builds 16 fewer table entries than it adds window products (~101 general products
@@ -686,6 +697,20 @@ fphe_status launch_encrypt27(fphe_ctx* c, const uint32_t* P, uint32_t lp, const 
 template <int L>
 fphe_status launch_decrypt27(fphe_ctx* c, const uint32_t* C, size_t count, uint32_t* P, hipStream_t s) {
   constexpr int TPI = L / 64, E = FPHE_WAVE / TPI, NL = rad_ll(TPI) * TPI, LH = L / 2, LQ = L / 4;
+  if (count <= wide_decrypt_max()) {
+    // few elements: one wave per (element, half) on the latency kernel (wide_dev.h), which
+    // writes the same y_s rows k_pow_half27 does; the CRT tail is the same kernel
+    const size_t ybytes = (size_t)ntiles_of(count) * 2 * LH * FPHE_WAVE * 4;
+    if (ensure_scratch(c, ybytes, s) != FPHE_OK) return FPHE_ERR_HIP;
+    u32* Y = c->scratch;
+    hipLaunchKernelGGL((k_pow_half_wide<L, kWinDec<TPI>>), dim3((unsigned)(2 * count)), dim3(64), 0, s, c->K, C, count, Y);
+    auto kcrt = k_decrypt_crt<L>;
+    const size_t lds2 = (size_t)kWavesPerBlock * LQ * FPHE_WAVE * 4;
+    set_lds(kcrt, lds2);
+    hipLaunchKernelGGL(kcrt, dim3(grid_for(c, count, bpc_for_slot(LQ))), dim3(kBlock), lds2, s, c->K, Y,
+                       ntiles_of(count), P);
+    return hip_ok(hipGetLastError());
+  }
   auto kern = KS<TPI>::template pow_half<L, kWinDec<TPI>, false>();
   const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
   set_lds(kern, lds);
