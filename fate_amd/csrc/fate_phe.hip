@@ -26,13 +26,14 @@ namespace {
 constexpr int kBlock = 256;      // 4 waves per workgroup
 constexpr int kWavesPerBlock = kBlock / FPHE_WAVE;
 // decryptions of at most this many elements run their half-size modexps on the one-element-
-// per-wave latency kernel (wide_dev.h k_pow_half_wide): below ~1 wave per SIMD of the
-// throughput kernel every wave of it runs alone at its per-row latency
+// per-wave latency kernel (wide_dev.h k_pow_half_wide): the throughput kernel takes ~25 ms for
+// anything up to ~32k elements (its waves run alone at their per-row latency), the latency
+// kernel 4.3 ms for up to ~300 and 10.9 ms for 2,048 (profiles/r05/r05g_latency_leg.txt)
 // (env FPHE_WIDE_DECRYPT_MAX overrides, read once: 0 turns the path off, for A/B and tests)
 inline size_t wide_decrypt_max() {
   static const size_t v = [] {
     const char* e = getenv("FPHE_WIDE_DECRYPT_MAX");
-    return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)2048;
+    return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)4096;
   }();
   return v;
 }

@@ -587,8 +587,8 @@ def test_large_key_vector_ops_and_pickle(bits, monkeypatch):
 
 @pytest.mark.parametrize("bits", [1024, 2048])
 def test_decrypt_latency_kernel_matches_throughput(bits):
-    """Decryptions of at most 2,048 elements run their half-size modexps on the one-element-
-    per-wave kernel (wide_dev.h k_pow_half_wide); 2,049 take the throughput kernel
+    """Decryptions of at most 4,096 elements run their half-size modexps on the one-element-
+    per-wave kernel (wide_dev.h k_pow_half_wide); 4,097 take the throughput kernel
     (k_pow_half27).  The same ciphertexts -- device-RNG encryptions of both signs, the edge
     values, and sums whose exponents were aligned -- decrypt to the same plaintexts either way,
     and the short ones round-trip to the encoded inputs."""
@@ -597,12 +597,12 @@ def test_decrypt_latency_kernel_matches_throughput(bits):
         fx = _json.load(f)
     sk, pk, coder = P.keypair_from_primes(int(fx["p"], 16), int(fx["q"], 16))
     g = torch.Generator().manual_seed(bits)
-    x = torch.randn(2049, generator=g, dtype=torch.float64) * 4
+    x = torch.randn(4097, generator=g, dtype=torch.float64) * 4
     x[:6] = torch.tensor([0.0, 1e-300, -1e-300, 1e300, -1e300, -1.0], dtype=torch.float64)
     xd = x.cuda()
     v = pk.encrypt_encoded(coder.encode_f64_vec(xd), True)
     v = v.add(pk, pk.encrypt_encoded(coder.encode_f64_vec(xd.flip(0) * 1e-3), True))
     big = sk.decrypt_to_encoded(v).to_ints()
-    for n in (2048, 37, 1):
+    for n in (4096, 37, 1):
         small = sk.decrypt_to_encoded(v.slice(0, n)).to_ints()
         assert small == (big[0][:n], big[1][:n]), n
