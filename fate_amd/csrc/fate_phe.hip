@@ -30,11 +30,18 @@ constexpr int kWavesPerBlock = kBlock / FPHE_WAVE;
 // anything up to ~32k elements (its waves run alone at their per-row latency), the latency
 // kernel 4.3 ms for up to ~300 and 10.9 ms for 2,048 (profiles/r05/r05g_latency_leg.txt)
 // (env FPHE_WIDE_DECRYPT_MAX overrides, read once: 0 turns the path off, for A/B and tests)
+inline size_t env_size(const char* name, size_t dflt) {
+  const char* e = getenv(name);
+  return e ? (size_t)strtoull(e, nullptr, 10) : dflt;
+}
 inline size_t wide_decrypt_max() {
-  static const size_t v = [] {
-    const char* e = getenv("FPHE_WIDE_DECRYPT_MAX");
-    return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)4096;
-  }();
+  static const size_t v = env_size("FPHE_WIDE_DECRYPT_MAX", 4096);
+  return v;
+}
+// obfuscated public-key encryptions of at most this many elements likewise (k_encrypt_wide):
+// the throughput kernel takes ~52 ms for anything up to ~16k elements (FPHE_WIDE_ENCRYPT_MAX)
+inline size_t wide_encrypt_max() {
+  static const size_t v = env_size("FPHE_WIDE_ENCRYPT_MAX", 2048);
   return v;
 }
 constexpr int kWinSlide = 6;     // sliding window of the 27-bit engine's shared-exponent modexps
@@ -673,10 +680,25 @@ fphe_status launch_encrypt27(fphe_ctx* c, const uint32_t* P, uint32_t lp, const 
   const size_t tbytes = (size_t)grid * kWavesPerBlock * kTabEntries<kWinSlide> * rad_ll(TPI) * FPHE_WAVE * 4;
   const size_t rbytes = (size_t)ntiles_of(m0) * L1 * FPHE_WAVE * 4;
   const bool draw = obf && !r;
-  if (ensure_scratch(c, tbytes + (draw ? rbytes : 0), s) != FPHE_OK) return FPHE_ERR_HIP;
   ChaChaKey ck;
   if (draw)
     for (int i = 0; i < 8; ++i) ck.k[i] = key[i];
+  if (obf && count <= wide_encrypt_max()) {
+    // few elements: one wave per element on the latency kernel (wide_dev.h), M-form written
+    // directly; r drawn as on the throughput path (element e's stream), so the integers agree
+    const size_t rb = (size_t)ntiles_of(count) * L1 * FPHE_WAVE * 4;
+    if (draw && ensure_scratch(c, rb, s) != FPHE_OK) return FPHE_ERR_HIP;
+    const u32* rbuf = r;
+    if (draw) {
+      const unsigned rgrid = (unsigned)std::min<size_t>((count + 255) / 256, (size_t)c->cus * 4);
+      hipLaunchKernelGGL(k_draw_r<L1>, dim3(rgrid), dim3(256), 0, s, c->K, count, ck, nonce, (size_t)0, c->scratch);
+      rbuf = c->scratch;
+    }
+    hipLaunchKernelGGL((k_encrypt_wide<L, kWinSlide>), dim3((unsigned)count), dim3(64), 0, s, c->K, P, lp, neg, count,
+                       rbuf, C, sign);
+    return hip_ok(hipGetLastError());
+  }
+  if (ensure_scratch(c, tbytes + (draw ? rbytes : 0), s) != FPHE_OK) return FPHE_ERR_HIP;
   for (size_t e0 = 0; e0 < count; e0 += span) {  // spans run in stream order over one scratch
     const size_t m = count - e0 < span ? count - e0 : span, t0 = e0 / FPHE_WAVE;
     const u32* rbuf = r ? r + t0 * L1 * FPHE_WAVE : nullptr;

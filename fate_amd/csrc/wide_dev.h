@@ -172,6 +172,21 @@ __device__ __forceinline__ void load_limbs(const u32* __restrict__ C, u32 rows, 
   }
 }
 
+// this lane's limbs of the number in the LDS word row wl (nwords words, then >= 2 zero words)
+template <int TPI>
+__device__ __forceinline__ void limbs_from_words(const u32* wl, u32 (&A)[TPI], int lane) {
+  using G = Geo<TPI>;
+#pragma unroll
+  for (int k = 0; k < TPI; ++k) {
+    u32 v = 0;
+    if (lane < G::NLANE) {
+      const u32 bit = (u32)(G::LB * (TPI * lane + k)), w = bit >> 5, off = bit & 31;
+      v = (u32)((((u64)wl[w + 1] << 32) | wl[w]) >> off) & G::MASK;
+    }
+    A[k] = v;
+  }
+}
+
 // this lane's limbs to an LDS row of NL limbs, and back
 template <int TPI>
 __device__ __forceinline__ void to_row(const u32 (&A)[TPI], u32* row_, int lane) {
@@ -361,4 +376,74 @@ __global__ __launch_bounds__(64) void k_pow_half_wide(KeyArgs K, const u32* __re
   for (int k = 0; k < TPI; ++k) Cst[k] = (lane == 0 && k == 0) ? 1u : 0u;
   wide::mul_reg<TPI>(A, Cst, N, np, lane);  // leave Montgomery form (< 2N)
   wide::store_limbs<TPI>(A, bl, S2, Y, 2 * L1, e, hq ? L1 : 0u, L1, lane);
+}
+
+// Obfuscated public-key encryption of few elements (k_encrypt27 + k_mont_const27 of the
+// throughput engine, same integers): one element per wave.  nude = 1 + m n mod n^2 with the
+// sign of m (paillier/src/lib.rs:104-121, the truncating %; m > n/4 encodes a negative integer
+// and 1 + m n is then the canonical inverse the reference takes), r^n by the sliding window
+// from r R, and M(C) = mont(r^n R, nude R) = C R straight into the Montgomery-resident form.
+// r: tile-major [.][L/2][64] (injected, or drawn by k_draw_r).
+template <int L, int W>
+__global__ __launch_bounds__(64) void k_encrypt_wide(KeyArgs K, const u32* __restrict__ P, u32 lp,
+                                                     const u8* __restrict__ neg, size_t count,
+                                                     const u32* __restrict__ R, u32* __restrict__ Co,
+                                                     u8* __restrict__ so) {
+  constexpr int TPI = L / 32;  // n^2: 148 limbs on 37 lanes for 2048-bit keys
+  using G = wide::Geo<TPI>;
+  constexpr int NL = G::NL;
+  constexpr u32 L1 = L / 2;
+  __shared__ u32 wl[L + 3];
+  __shared__ u32 bl[NL + 3];
+  __shared__ u32 tab[(1 << (W - 1)) * NL];
+  __shared__ u32 mneg_s;
+  const int lane = (int)threadIdx.x;
+  const size_t e = blockIdx.x;
+  if (e >= count) return;  // block-uniform
+  u32 N[TPI], A[TPI], Nd[TPI], Cst[TPI];
+  wide::const_limbs<TPI>(K.N2_27, N, lane);
+  const u32 np = K.n2_np27;
+  // the nude ciphertext in 32-bit words (as nude_to_slot), on lane 0
+  for (u32 w = (u32)lane; w < L + 3; w += 64) wl[w] = 0u;
+  __syncthreads();
+  if (lane == 0) {
+    const u32* pe = P + (e >> 6) * (size_t)lp * 64 + (e & 63);
+    u32 any = 0;
+    for (u32 k = 0; k < lp; ++k) {
+      const u32 pk = pe[(size_t)k * 64];
+      any |= pk;
+      u64 acc = 0;
+      for (u32 j = 0; j < L1; ++j) {
+        acc = (u64)pk * K.n[j] + wl[k + j] + (acc >> 32);
+        wl[k + j] = (u32)acc;
+      }
+      wl[k + L1] = (u32)(acc >> 32);
+    }
+    const bool mneg = neg[e] != 0 && any != 0;
+    if (mneg) {  // n^2 - |m| n
+      u32 br = 0;
+      for (u32 j = 0; j < L; ++j) {
+        const u64 d = (u64)K.N2[j] - wl[j] - br;
+        wl[j] = (u32)d;
+        br = (u32)(d >> 63);
+      }
+    }
+    u32 c = 1;  // + 1
+    for (u32 j = 0; j < L && c; ++j) {
+      const u64 t = (u64)wl[j] + c;
+      wl[j] = (u32)t;
+      c = (u32)(t >> 32);
+    }
+    mneg_s = mneg ? 1u : 0u;
+  }
+  __syncthreads();
+  wide::limbs_from_words<TPI>(wl, Nd, lane);
+  wide::load_limbs<TPI>(R, L1, e, 0, wl, A, lane);  // r < n
+  wide::const_limbs<TPI>(K.N2R2_27, Cst, lane);
+  wide::mul_reg<TPI>(A, Cst, N, np, lane);   // r R
+  wide::mul_reg<TPI>(Nd, Cst, N, np, lane);  // nude R
+  wide::powm<TPI, W>(A, tab, N, np, K.n, K.nbits, lane);  // r^n R
+  wide::mul_reg<TPI>(A, Nd, N, np, lane);    // r^n nude R = M(C), < 2N
+  wide::store_limbs<TPI>(A, bl, K.N2_27, Co, L, e, 0, L, lane);
+  if (lane == 0) so[e] = (u8)mneg_s;
 }

@@ -606,3 +606,31 @@ def test_decrypt_latency_kernel_matches_throughput(bits):
     for n in (4096, 37, 1):
         small = sk.decrypt_to_encoded(v.slice(0, n)).to_ints()
         assert small == (big[0][:n], big[1][:n]), n
+
+
+@pytest.mark.parametrize("bits", [1024, 2048])
+def test_encrypt_latency_kernel_matches_throughput(bits):
+    """Obfuscated public-key encryptions of at most 2,048 elements run on the one-element-per-
+    wave kernel (wide_dev.h k_encrypt_wide, M-form written directly); 2,049 take k_encrypt27 +
+    k_mont_const27.  With the same injected r the integers agree, for float significands of
+    both signs (negative ciphertexts), zero, and encoded negative integers (m > n/4); the short
+    ones also decrypt to their significands."""
+    import json as _json
+    import random as _random
+    with open(os.path.join(HERE, "golden", f"paillier_{bits}.json")) as f:
+        fx = _json.load(f)
+    sk, pk, coder = P.keypair_from_primes(int(fx["p"], 16), int(fx["q"], 16), keyholder=False)
+    rng = _random.Random(bits)
+    n = 2049
+    x = torch.tensor([rng.uniform(-5, 5) for _ in range(n)], dtype=torch.float64)
+    x[:3] = torch.tensor([0.0, -1e-300, 1e300], dtype=torch.float64)
+    pv = coder.encode_f64_vec(x.cuda())
+    iv = coder.encode_i64_vec(torch.tensor([-7, 5, -(1 << 40)] * 683, dtype=torch.int64).cuda())
+    rs = [1 + rng.randrange(pk.n - 1) for _ in range(n)]
+    for v in (pv, iv):
+        big = pk.encrypt_encoded(v, True, r=rs).to_signed_ints(pk.ns)
+        for m in (2048, 5, 1):
+            sub = v._gather(torch.arange(m))
+            small = pk.encrypt_encoded(sub, True, r=rs[:m])
+            assert small.to_signed_ints(pk.ns) == (big[0][:m], big[1][:m]), m
+        assert sk.decrypt_to_encoded(small).to_ints()[0] == [s_ % pk.n for s_ in v._gather(torch.arange(1)).to_ints()[0]]

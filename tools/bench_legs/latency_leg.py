@@ -19,7 +19,7 @@ def run(mode: str) -> dict:
     import torch
     from fate_amd import paillier as P
     fx = json.load(open(os.path.join(ROOT, "tests", "golden", "paillier_2048.json")))
-    sk, pk, coder = P.keypair_from_primes(int(fx["p"], 16), int(fx["q"], 16))
+    sk, pk, coder = P.keypair_from_primes(int(fx["p"], 16), int(fx["q"], 16), keyholder=False)
     dev = torch.device("cuda", 0)
     if mode == "throughput":
         P.WIDE_SQUEEZE_MAX_CHUNKS = 0
@@ -38,6 +38,17 @@ def run(mode: str) -> dict:
             ts.append(time.perf_counter() - t0)
         out[f"decrypt_{n}_ms"] = round(min(ts) * 1e3, 3)
         out[f"decrypt_{n}_ok"] = bool(torch.allclose(coder.decode_f64_vec(d), x[:n], rtol=0, atol=0))
+    for n in (1, 16, 256, 2048):
+        xe = coder.encode_f64_vec(x[:n])
+        pk.encrypt_encoded(xe, True)  # warm
+        torch.cuda.synchronize(dev)
+        ts = []
+        for _ in range(2):
+            t0 = time.perf_counter()
+            pk.encrypt_encoded(xe, True)
+            torch.cuda.synchronize(dev)
+            ts.append(time.perf_counter() - t0)
+        out[f"encrypt_{n}_ms"] = round(min(ts) * 1e3, 3)
     for slots, shift in ((128, 148), (320, 154)):
         s = v.slice(0, slots)
         s.pack_squeeze(13, shift, pk)
@@ -56,7 +67,7 @@ if __name__ == "__main__":
     if len(sys.argv) > 1:
         print(json.dumps(run(sys.argv[1])), flush=True)
     else:
-        for mode, env in (("wide", {}), ("throughput", {"FPHE_WIDE_DECRYPT_MAX": "0"})):
+        for mode, env in (("wide", {}), ("throughput", {"FPHE_WIDE_DECRYPT_MAX": "0", "FPHE_WIDE_ENCRYPT_MAX": "0"})):
             r = subprocess.run([sys.executable, os.path.abspath(__file__), mode], env={**os.environ, **env},
                                capture_output=True, text=True, timeout=600)
             line = [l for l in r.stdout.splitlines() if l.startswith("{")]
