@@ -101,18 +101,29 @@ def enc_mad27_per_elem(key_bits: int, n: int) -> float:
     return (1 + mul + 1) * 2 * NL * NL + sq * NL * TPI * (ENGINE_LL // 2 + 1 + ENGINE_LL)
 
 
-def enc_crt_mac32_per_elem(key_bits: int) -> float:
+def kh_direct_z(p: int, q: int) -> bool:
+    """Whether the library draws the key holder's obfuscation as (z_p, z_q) directly
+    (k_draw_z): FPHE_KH_DIRECT_Z unset or nonzero, and gcd(q, p-1) =
+    gcd(p, q-1) = 1 (p, q prime: neither divides the other's predecessor)."""
+    return os.environ.get("FPHE_KH_DIRECT_Z", "1") != "0" and (p - 1) % q != 0 and (q - 1) % p != 0
+
+
+def enc_crt_mac32_per_elem(key_bits: int, direct: bool = True) -> float:
     # key-holder encrypt, the w=5 fixed-window formula of SURVEY.md §8(d) for the modexps it
-    # runs, + 4 products of the recombination over n^2.  Keys above 1024 bits (the split,
-    # FPHE_KH_SPLIT): per half z = r^(q mod (p-1)) mod p over the key/64-limb p,
-    # then z^p mod p^2 over the key/32-limb p^2, both with (key/2)-bit exponents; up to 1024
-    # bits: one (n mod s(s-1))-bit (~key_bits) exponent mod s^2 per half
+    # runs, + 4 products of the recombination over n^2.  With the direct draw (k_draw_z,
+    # any key size): per half z^p mod p^2 over the key/32-limb p^2, a (key/2)-bit exponent.
+    # Otherwise, keys above 1024 bits (the split, FPHE_KH_SPLIT, DESIGN.md §3): per half z =
+    # r^(q mod (p-1)) mod p over the key/64-limb p first; up to 1024 bits: one (n mod
+    # s(s-1))-bit (~key_bits) exponent mod s^2 per half
+    rec = 4 * mac32_per_mont(key_bits // 16)
+    E = key_bits // 2
+    if direct:
+        return 2 * (E + math.ceil(E / 5) + 16) * mac32_per_mont(key_bits // 32) + rec
     if key_bits > 1024:
-        E = key_bits // 2
         per_half = (E + math.ceil(E / 5) + 16) * (mac32_per_mont(key_bits // 64) + mac32_per_mont(key_bits // 32))
-        return 2 * per_half + 4 * mac32_per_mont(key_bits // 16)
+        return 2 * per_half + rec
     E = key_bits
-    return 2 * (E + math.ceil(E / 5) + 16) * mac32_per_mont(key_bits // 32) + 4 * mac32_per_mont(key_bits // 16)
+    return 2 * (E + math.ceil(E / 5) + 16) * mac32_per_mont(key_bits // 32) + rec
 
 
 def dec_mac32_per_elem(key_bits: int) -> float:
@@ -979,8 +990,9 @@ def main() -> None:
         del ck, yk, cpub, ckh
         extras = {
             "encrypt_keyholder_crt_per_s": round(N / (crt_ms / 1e3), 1),
-            "encrypt_keyholder_crt_roofline_frac": round(N * enc_crt_mac32_per_elem(key_bits) / (crt_ms / 1e3) / 1e12
-                                                         / PEAK_TMAC32, 4),
+            "encrypt_keyholder_crt_roofline_frac": round(N * enc_crt_mac32_per_elem(key_bits, kh_direct_z(sk.p, sk.q))
+                                                         / (crt_ms / 1e3) / 1e12 / PEAK_TMAC32, 4),
+            "encrypt_keyholder_direct_z": kh_direct_z(sk.p, sk.q),
             "encrypt_keyholder_crt_roundtrip_bit_exact": crt_roundtrip,
             "encrypt_keyholder_crt_equals_public_4096": crt_same,
             "ct_mul_per_s": round(N / (mul_ms / 1e3), 1),

@@ -38,6 +38,12 @@ inline size_t wide_decrypt_max() {
   static const size_t v = env_size("FPHE_WIDE_DECRYPT_MAX", 4096);
   return v;
 }
+// the key holder's device-drawn obfuscation in CRT coordinates (k_draw_z); FPHE_KH_DIRECT_Z=0:
+// r and the two-step modexp as for injected r (A/B)
+inline bool kh_direct_z() {
+  static const bool v = env_size("FPHE_KH_DIRECT_Z", 1) != 0;
+  return v;
+}
 // obfuscated public-key encryptions of at most this many elements likewise (k_encrypt_wide):
 // the throughput kernel takes ~52 ms for anything up to ~16k elements (FPHE_WIDE_ENCRYPT_MAX)
 inline size_t wide_encrypt_max() {
@@ -259,6 +265,79 @@ __global__ __launch_bounds__(256) void k_draw_r(KeyArgs K, size_t count, ChaChaK
     draw_r<L1>(r, K, ck, nonce, ebase + e);
 #pragma unroll
     for (int j = 0; j < L1; ++j) R[tiled(e, L1, j)] = r[j];
+  }
+}
+
+// Key-holder obfuscation drawn in its CRT coordinates.  The split modexp (k_pow_small27, then
+// k_pow_half27<., ., true>) turns r into z_p = r^(q mod (p-1)) mod p and z_q likewise, then
+// raises z_s to s mod s^2.  For r uniform in Z_n^*, (r mod p, r mod q) is uniform in
+// Z_p^* x Z_q^*, and x -> x^q is a bijection of Z_p^* when gcd(q, p - 1) = 1 (x -> x^p of Z_q^*
+// likewise): so (z_p, z_q) is uniform in Z_p^* x Z_q^*, and drawing it directly gives r^n mod
+// n^2 with the distribution of the reference's random_rn (paillier/src/lib.rs:94-98;
+// random.rs:22-25, r in [1, n-1]: the r sharing a factor with n, probability < 2^-1000, aside)
+// for the cost of the second step only.  Injected r (parity mode) keeps the two-step path.
+// z_s uniform in [1, s-1] from element e's ChaCha20 stream of half h (nonce tweaked per half,
+// so the streams are disjoint from each other and from draw_r's); rows of Z as k_pow_small27
+// writes them.
+template <int LQ>
+__device__ __forceinline__ void draw_below(u32 (&A)[LQ], const u32* __restrict__ sm1, int sbits, const ChaChaKey& ck,
+                                           u64 nonce, size_t e) {
+  constexpr int NB = (LQ + 15) / 16;
+  auto wmask = [&](int j) -> u32 {
+    const int b = sbits - 32 * j;
+    return b >= 32 ? 0xffffffffu : (b <= 0 ? 0u : ((1u << b) - 1u));
+  };
+  bool done = false;
+  u32 attempt = 0;
+  while (__any(!done)) {
+    if (!done) {
+      u32 x[LQ];
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        u32 blk[16];
+        chacha20_block(ck, (attempt * NB + b) | ((u32)(e >> 32) << 16), (u32)e, (u32)(nonce >> 32), (u32)nonce,
+                       blk);
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (b * 16 + i < LQ) x[b * 16 + i] = blk[i];
+      }
+#pragma unroll
+      for (int j = 0; j < LQ; ++j) x[j] &= wmask(j);
+      u32 br = 0;  // accept iff x < s - 1, then z = x + 1 in [1, s - 1]
+#pragma unroll
+      for (int j = 0; j < LQ; ++j) {
+        const u64 d = (u64)x[j] - sm1[j] - br;
+        br = (u32)(d >> 63);
+      }
+      if (br) {
+        u32 c = 1;
+#pragma unroll
+        for (int j = 0; j < LQ; ++j) {
+          const u64 t = (u64)x[j] + c;
+          A[j] = (u32)t;
+          c = (u32)(t >> 32);
+        }
+        done = true;
+      }
+    }
+    ++attempt;
+  }
+}
+
+template <int L>
+__global__ __launch_bounds__(256) void k_draw_z(KeyArgs K, size_t count, ChaChaKey ck, u64 nonce, size_t ebase,
+                                                 u32* __restrict__ Z) {
+  constexpr int LQ = L / 4;
+  constexpr u32 ZW = 32u * (L >= 128 ? L / 128 : 1);  // kZWords<L> (kernels27.h): z_s words per half
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < count; e += (size_t)gridDim.x * blockDim.x) {
+#pragma unroll 1
+    for (u32 h = 0; h < 2; ++h) {
+      u32 z[LQ];
+      draw_below<LQ>(z, h ? K.qm1 : K.pm1, h ? K.q_bits : K.p_bits, ck,
+                     nonce ^ (0x9E3779B97F4A7C15ull * (h + 1)), ebase + e);
+#pragma unroll
+      for (u32 j = 0; j < ZW; ++j) Z[tiled(e, 2 * ZW, h * ZW + j)] = j < (u32)LQ ? z[j] : 0u;
+    }
   }
 }
 
@@ -558,6 +637,9 @@ struct fphe_ctx {
   // stream reads back the exponent range and sorts the terms
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // the key holder may draw its obfuscation as (z_p, z_q) directly (k_draw_z): set when
+  // gcd(q, p - 1) = gcd(p, q - 1) = 1, which makes r -> (z_p, z_q) a bijection
+  bool kh_direct = false;
   std::mutex mu;
 };
 
@@ -780,12 +862,17 @@ fphe_status launch_encrypt_crt27(fphe_ctx* c, const uint32_t* P, uint32_t lp, co
   const size_t lds0 = (size_t)kWavesPerBlock * NLs * Es * 4;
   unsigned g0 = 0;
   size_t zbytes = 0;
+  const bool direct = !r && c->kh_direct && kh_direct_z();
   if (kKhSplit<L>) {
     set_lds(k0, lds0);
     g0 = occ_grid(c, k0, lds0, (m0 + Es - 1) / Es, "pow_small27");
     tbytes = std::max(tbytes, (size_t)g0 * kWavesPerBlock * kTabEntries<kWinSlide> * rad_ll(TPIs) * FPHE_WAVE * 4);
-    zbytes = (size_t)ntiles_of(m0) * 2 * kZWords<L> * FPHE_WAVE * 4;
   }
+  if (kKhSplit<L> || direct) zbytes = (size_t)ntiles_of(m0) * 2 * kZWords<L> * FPHE_WAVE * 4;
+  // the second step alone on drawn (z_p, z_q): k1 itself when the key splits its modexp,
+  // otherwise (keys <= 1024 bits) the same kernel reading Z (|p|-bit exponent in place of |n|)
+  auto k1z = KS<TPIh>::template pow_half_z<L, kWinSlide>();
+  if (direct && !kKhSplit<L>) set_lds(k1z, lds1);
   const size_t ybytes = (size_t)ntiles_of(m0) * 2 * L1 * FPHE_WAVE * 4;
   const size_t rbytes = (size_t)ntiles_of(m0) * L1 * FPHE_WAVE * 4;
   if (ensure_scratch(c, tbytes + ybytes + zbytes + (r ? 0 : rbytes), s) != FPHE_OK) return FPHE_ERR_HIP;
@@ -801,9 +888,17 @@ fphe_status launch_encrypt_crt27(fphe_ctx* c, const uint32_t* P, uint32_t lp, co
   for (size_t e0 = 0; e0 < count; e0 += span) {
     const size_t m = count - e0 < span ? count - e0 : span, t0 = e0 / FPHE_WAVE;
     const u32* rbuf = r ? r + t0 * L1 * FPHE_WAVE : nullptr;
+    const unsigned rgrid = (unsigned)std::min<size_t>((m + 255) / 256, (size_t)c->cus * 4);
+    if (direct) {  // (z_p, z_q) drawn in place of r and its first modexp step
+      hipLaunchKernelGGL(k_draw_z<L>, dim3(rgrid), dim3(256), 0, s, c->K, m, ck, nonce, e0, Z);
+      hipLaunchKernelGGL(k1z, dim3(g1), dim3(kBlock), lds1, s, c->K, (const u32*)Z, m, Y, c->scratch, (u32)NLh);
+      hipLaunchKernelGGL(k2, dim3(g2), dim3(kBlock), lds2, s, c->K, P + t0 * lp * FPHE_WAVE, lp, neg + e0, m, Y,
+                         C + t0 * L * FPHE_WAVE, sign + e0, (u32)LDSW);
+      if (hipGetLastError() != hipSuccess) return FPHE_ERR_HIP;
+      continue;
+    }
     if (!r) {
       u32* rdev = Z + zbytes / 4;
-      const unsigned rgrid = (unsigned)std::min<size_t>((m + 255) / 256, (size_t)c->cus * 4);
       hipLaunchKernelGGL(k_draw_r<L1>, dim3(rgrid), dim3(256), 0, s, c->K, m, ck, nonce, e0, rdev);
       rbuf = rdev;
     }
@@ -1719,6 +1814,7 @@ fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, 
     size_t o_Ps = 0, o_PsR2 = 0, o_PsR3 = 0, o_Qs = 0, o_QsR2 = 0, o_QsR3 = 0, o_e1p = 0, o_e1q = 0;
     u32 ps_np = 0, qs_np = 0;
     int e1pb = 0, e1qb = 0, pb = 0, qb = 0;
+    bool kh_direct = false;
     const bool has_sk = p_w != nullptr;
     if (has_sk) {
       Limbs p = from_words(p_w, LQ), q = from_words(q_w, LQ);
@@ -1785,6 +1881,8 @@ fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, 
         o_e1q = put(e1q, LQ);
         e1pb = (int)hbn::bitlen(e1p); e1qb = (int)hbn::bitlen(e1q);
         pb = (int)hbn::bitlen(p); qb = (int)hbn::bitlen(q);
+        // p, q prime: gcd(q, p - 1) = 1 iff q does not divide p - 1 (and likewise)
+        kh_direct = !hbn::is_zero(hbn::mod(pm1, q)) && !hbn::is_zero(hbn::mod(qm1, p));
       }
       const Limbs R27 = hbn::pow2_mod((size_t)LB2 * NL2, N2);
       const Limbs Kp = hbn::mul(Q2, hbn::inv_mod(hbn::mod(Q2, P2), P2));  // < n^2
@@ -1794,6 +1892,7 @@ fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, 
     }
     auto* c = new fphe_ctx();
     c->device = device; c->key_bits = key_bits; c->L1 = L1; c->L2 = L2; c->LQ = LQ; c->has_sk = has_sk;
+    c->kh_direct = has_sk && kh_direct;
     DevGuard g(device);
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) { delete c; return FPHE_ERR_HIP; }
