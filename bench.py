@@ -1016,7 +1016,7 @@ def main() -> None:
             "roundtrip_bit_exact": roundtrip_ok,
             "decrypt_roofline_frac": round(N * dec_mac32_per_elem(key_bits) / (dec_ms / 1e3) / 1e12 / PEAK_TMAC32, 4),
             "rooflines": {
-                "decrypt": valu_roofline("k_pow_half27<128,6,false> + k_decrypt_crt<128>",
+                "decrypt": valu_roofline("k_pow_half27<128,6,false,false> + k_decrypt_crt<128>",
                                          N * dec_mac32_per_elem(key_bits), dec_ms,
                                          N * (key_bits // 4 + 4 + key_bits // 8),
                                          traffic=_traffic("decrypt", N), traffic_source=pmc_ops_traffic("decrypt")[1],

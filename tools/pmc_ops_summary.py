@@ -1,6 +1,6 @@
 """HBM traffic of the decrypt, ct-add, ct x pt and iupdate kernels from FETCH_SIZE / WRITE_SIZE
 passes over tools/bench_legs/ops_pmc_leg.py (tools/gpu_job.sh pmc): decrypt of 2^18 elements
-(k_pow_half27<128, 6, false> + k_decrypt_crt<128>), the Hetero-LR-shaped ct-add of 2^20
+(k_pow_half27<128, 6, false, false> + k_decrypt_crt<128>), the Hetero-LR-shaped ct-add of 2^20
 (k_add27<128>), ct x pt of 2^18 (classify, batch inverse, k_mul27), the histogram fold's copy
 and balanced level over 8.4M terms, 2048-bit key.  The counters are scaled per kernel by the
 calibration probe's factors for that kernel's access pattern (CAL below).  bench.py reports the result as the
@@ -13,7 +13,7 @@ import csv
 import json
 import sys
 
-KERNELS = {"decrypt": (["k_pow_half27<128, 6, false>", "k_decrypt_crt<128>"], 1 << 18,
+KERNELS = {"decrypt": (["k_pow_half27<128, 6, false, false>", "k_decrypt_crt<128>"], 1 << 18,
                        "algorithmic: read 512 B C (+ sign/exp), write 4-256 B plaintext"),
            "ct_add": (["k_add27<128>"], 1 << 20, "algorithmic: two 517-B operands read, one written (+4-B order)"),
            "ct_mul": (["k_mul_prep<128>", "k_binv_pre27<128>", "k_inv_n27<128>", "k_inv_lift27<128>",
