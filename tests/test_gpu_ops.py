@@ -420,3 +420,39 @@ def test_neg_batch_inversion_full_grid(env):
     C = prod.C.transpose(1, 2).reshape(-1, prod.L2)[:n]  # tile-major [tiles][L2][64] -> rows
     assert bool((C == pk._key.mont_one(C.device)).all())  # M(1): the integer 1 in Montgomery form
     assert torch.equal(prod.exp[:n], a.exp[:n])
+
+
+def test_empty_and_degenerate_vector_ops(env):
+    """Empty and degenerate inputs through the vector algebra, against the oracle's loops on
+    the same inputs (lib.rs:439-450, :724-791, :852-908): iupdate with no terms and with
+    every sample's index list empty, a zero-size chunk and a step past its chunk in
+    chunking_cumsum_with_step, empty intervals, pack_squeeze of nothing, matmul / rmatmul
+    with a zero inner or outer dimension (the literal-1 zeros), decrypt of nothing."""
+    fx, sk, pk, coder, opk, cts = env
+    data = more(opk, cts, 12, 5)
+    empty = dev_vec(pk, [])
+    v = dev_vec(pk, data)
+    v.iupdate(empty, [], 1, pk)
+    assert host(pk, v) == ref(data)
+    v.iupdate(dev_vec(pk, data[:6]), [[]] * 6, 2, pk)
+    want = list(data)
+    O.iupdate(opk, want, data[:6], [[]] * 6, 2)
+    assert host(pk, v) == ref(want)
+    for sizes, step in (([0, 5, 0, 7], 2), ([3, 9], 4), ([12], 12), ([], 1)):
+        v = dev_vec(pk, data)
+        v.chunking_cumsum_with_step(pk, sizes, step)
+        want = list(data)
+        O.chunking_cumsum_with_step(opk, want, sizes, step)
+        assert host(pk, v) == ref(want), (sizes, step)
+    got = dev_vec(pk, data).intervals_sum_with_step(pk, [(4, 4), (0, 0)], 2)
+    assert host(pk, got) == ref(O.intervals_sum_with_step(opk, data, [(4, 4), (0, 0)], 2))
+    assert host(pk, empty.pack_squeeze(3, 20, pk)) == []
+    pv0 = P.PlaintextVector.from_ints([], [])
+    got = dev_vec(pk, []).matmul(pk, pv0, [3, 0], [0, 2])
+    assert host(pk, got) == ref(O.matmul(opk, [], [], [3, 0], [0, 2]))
+    bs = [O.encode_f64(opk.n, 1.5 - k) for k in range(8)]
+    pv = P.PlaintextVector.from_ints([b.significant for b in bs], [b.exp for b in bs])
+    assert host(pk, empty.matmul(pk, pv, [0, 4], [4, 2])) == []
+    got = dev_vec(pk, []).rmatmul(pk, pv0, [0, 3], [2, 0])
+    assert host(pk, got) == ref(O.rmatmul(opk, [], [], [0, 3], [2, 0]))
+    assert sk.decrypt_to_encoded(empty).to_ints() == ([], [])
