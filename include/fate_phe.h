@@ -150,7 +150,11 @@ fphe_status fphe_encrypt(fphe_ctx* ctx, const uint32_t* P, uint32_t lp, const ui
  * half-width modexps (about half the multiply work).  FATE's encrypting parties
  * (Hetero-LR / SecureBoost guest, arch/context/_cipher.py) hold the private key they
  * generated.  Requires a context created with p, q (else FPHE_ERR_NO_SK); r and rng_*
- * as fphe_encrypt. */
+ * as fphe_encrypt.  With r == NULL (device-drawn obfuscation) the library draws
+ * z_p (standing for r^q mod p) and z_q (for r^p mod q) uniformly in Z_p^* x Z_q^* instead
+ * of r and runs only z^s mod s^2 per half: the same distribution of r^n mod n^2 whenever
+ * gcd(q, p-1) = gcd(p, q-1) = 1, checked at context creation (env
+ * FPHE_KH_DIRECT_Z=0 draws r instead).  An injected r always gives the integers above. */
 fphe_status fphe_encrypt_crt(fphe_ctx* ctx, const uint32_t* P, uint32_t lp, const uint8_t* neg,
                              size_t count, const uint32_t* r, const uint32_t rng_key[8],
                              uint64_t rng_nonce, uint32_t* C, uint8_t* sign, void* stream);
