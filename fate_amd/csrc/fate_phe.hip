@@ -44,6 +44,12 @@ inline bool kh_direct_z() {
   static const bool v = env_size("FPHE_KH_DIRECT_Z", 1) != 0;
   return v;
 }
+// key-holder encryptions with drawn (z_p, z_q) of at most this many elements run their
+// z^s mod s^2 halves on the latency kernel (k_pow_half_enc_wide, decrypt's chain shape)
+inline size_t wide_kh_encrypt_max() {
+  static const size_t v = env_size("FPHE_WIDE_KH_ENCRYPT_MAX", 4096);
+  return v;
+}
 // obfuscated public-key encryptions of at most this many elements likewise (k_encrypt_wide):
 // the throughput kernel takes ~52 ms for anything up to ~16k elements (FPHE_WIDE_ENCRYPT_MAX)
 inline size_t wide_encrypt_max() {
@@ -891,7 +897,11 @@ fphe_status launch_encrypt_crt27(fphe_ctx* c, const uint32_t* P, uint32_t lp, co
     const unsigned rgrid = (unsigned)std::min<size_t>((m + 255) / 256, (size_t)c->cus * 4);
     if (direct) {  // (z_p, z_q) drawn in place of r and its first modexp step
       hipLaunchKernelGGL(k_draw_z<L>, dim3(rgrid), dim3(256), 0, s, c->K, m, ck, nonce, e0, Z);
-      hipLaunchKernelGGL(k1z, dim3(g1), dim3(kBlock), lds1, s, c->K, (const u32*)Z, m, Y, c->scratch, (u32)NLh);
+      if (count <= wide_kh_encrypt_max())  // few elements: one per wave and half
+        hipLaunchKernelGGL((k_pow_half_enc_wide<L, kWinDec<TPIh>>), dim3((unsigned)(2 * m)), dim3(64), 0, s, c->K,
+                           (const u32*)Z, m, Y);
+      else
+        hipLaunchKernelGGL(k1z, dim3(g1), dim3(kBlock), lds1, s, c->K, (const u32*)Z, m, Y, c->scratch, (u32)NLh);
       hipLaunchKernelGGL(k2, dim3(g2), dim3(kBlock), lds2, s, c->K, P + t0 * lp * FPHE_WAVE, lp, neg + e0, m, Y,
                          C + t0 * L * FPHE_WAVE, sign + e0, (u32)LDSW);
       if (hipGetLastError() != hipSuccess) return FPHE_ERR_HIP;

@@ -378,6 +378,44 @@ __global__ __launch_bounds__(64) void k_pow_half_wide(KeyArgs K, const u32* __re
   wide::store_limbs<TPI>(A, bl, S2, Y, 2 * L1, e, hq ? L1 : 0u, L1, lane);
 }
 
+// The key holder's half-size modexps for few elements (k_pow_half27<L, W, true, true> of the
+// throughput engine, same inputs and outputs): block 2e + h raises element e's drawn z_s
+// (k_draw_z: words [h ZW, h ZW + ZW) of Z[tile][2 ZW][64], z_s < s) to x_s = z_s^s mod s^2,
+// canonical, into Y rows [h L1, h L1 + L1); k_encrypt_crt27 recombines.  The chain is decrypt's
+// (a |s|-bit exponent mod s^2) without the c mod s^2 prologue.
+template <int L, int W>
+__global__ __launch_bounds__(64) void k_pow_half_enc_wide(KeyArgs K, const u32* __restrict__ Z, size_t count,
+                                                          u32* __restrict__ Y) {
+  constexpr int TPI = L / 64;
+  using G = wide::Geo<TPI>;
+  constexpr int NL = G::NL;
+  constexpr u32 L1 = L / 2, ZW = 32u * (L >= 128 ? L / 128 : 1);  // kZWords<L>
+  __shared__ u32 wl[L + 3];
+  __shared__ u32 bl[NL + 3];
+  __shared__ u32 tab[(1 << (W - 1)) * NL];
+  const int lane = (int)threadIdx.x;
+  const size_t e = blockIdx.x >> 1;
+  const u32 h = blockIdx.x & 1u;
+  if (e >= count) return;  // block-uniform
+  const u32* S2 = h ? K.Q2_27 : K.P2_27;
+  const u32 np = h ? K.q2_np27 : K.p2_np27;
+  u32 N[TPI], A[TPI], Cst[TPI];
+  wide::const_limbs<TPI>(S2, N, lane);
+  // this half's ZW words only (the other half's follow them in the element's rows)
+  __syncthreads();
+  const u32* src = Z + (e >> 6) * (size_t)(2 * ZW) * 64 + (e & 63) + (size_t)h * ZW * 64;
+  for (u32 w = (u32)lane; w < L + 3; w += 64) wl[w] = w < ZW ? src[(size_t)w * 64] : 0u;
+  __syncthreads();
+  wide::limbs_from_words<TPI>(wl, A, lane);
+  wide::const_limbs<TPI>(h ? K.Q2R2_27 : K.P2R2_27, Cst, lane);
+  wide::mul_reg<TPI>(A, Cst, N, np, lane);  // z R_s
+  wide::powm<TPI, W>(A, tab, N, np, h ? K.q : K.p, h ? K.q_bits : K.p_bits, lane);
+#pragma unroll
+  for (int k = 0; k < TPI; ++k) Cst[k] = (lane == 0 && k == 0) ? 1u : 0u;
+  wide::mul_reg<TPI>(A, Cst, N, np, lane);  // leave Montgomery form (< 2N)
+  wide::store_limbs<TPI>(A, bl, S2, Y, 2 * L1, e, h ? L1 : 0u, L1, lane);
+}
+
 // Obfuscated public-key encryption of few elements (k_encrypt27 + k_mont_const27 of the
 // throughput engine, same integers): one element per wave.  nude = 1 + m n mod n^2 with the
 // sign of m (paillier/src/lib.rs:104-121, the truncating %; m > n/4 encodes a negative integer

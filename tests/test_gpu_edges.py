@@ -634,3 +634,28 @@ def test_encrypt_latency_kernel_matches_throughput(bits):
             small = pk.encrypt_encoded(sub, True, r=rs[:m])
             assert small.to_signed_ints(pk.ns) == (big[0][:m], big[1][:m]), m
         assert sk.decrypt_to_encoded(small).to_ints()[0] == [s_ % pk.n for s_ in v._gather(torch.arange(1)).to_ints()[0]]
+
+
+@pytest.mark.parametrize("bits", [1024, 2048])
+def test_keyholder_encrypt_latency_kernel_matches_throughput(monkeypatch, bits):
+    """Key-holder encryptions with device-drawn (z_p, z_q) of at most 4,096 elements raise
+    z_s^s mod s^2 on the one-element-per-wave kernel (wide_dev.h k_pow_half_enc_wide); 4,097
+    take k_pow_half27<., ., true, true>.  With the nonce fixed, element i draws the same
+    (z_p, z_q) in both calls (its index's stream), so the ciphertexts agree; they decrypt to
+    the significands."""
+    import json as _json
+    with open(os.path.join(HERE, "golden", f"paillier_{bits}.json")) as f:
+        fx = _json.load(f)
+    sk, pk, coder = P.keypair_from_primes(int(fx["p"], 16), int(fx["q"], 16))
+    assert pk.keyholder
+    monkeypatch.setattr(pk._priv, "next_nonce", lambda: 777)
+    n = 4097
+    x = (torch.randn(n, generator=torch.Generator().manual_seed(bits), dtype=torch.float64) * 3).cuda()
+    x[:2] = torch.tensor([0.0, -2.5], dtype=torch.float64)
+    pv = coder.encode_f64_vec(x)
+    big = pk.encrypt_encoded(pv, True).to_signed_ints(pk.ns)
+    for m in (4096, 37, 1):
+        small = pk.encrypt_encoded(pv._gather(torch.arange(m)), True)
+        assert small.to_signed_ints(pk.ns) == (big[0][:m], big[1][:m]), m
+    got = coder.decode_f64_vec(sk.decrypt_to_encoded(small)).cpu()
+    assert got.tolist() == x[:1].cpu().tolist()
