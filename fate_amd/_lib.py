@@ -38,7 +38,7 @@ EXPORTED_SYMBOLS = (
     "fphe_encrypt", "fphe_encrypt_crt", "fphe_decrypt", "fphe_add", "fphe_add_ordered", "fphe_add_order", "fphe_mul", "fphe_neg", "fphe_sqmul", "fphe_align",
     "fphe_fold", "fphe_fold_segments", "fphe_permute", "fphe_export_signed", "fphe_import_signed",
     "fphe_wire_lengths", "fphe_wire_encode", "fphe_wire_scan", "fphe_wire_decode", "fphe_chacha20_blocks",
-    "fphe_clock_stamp", "fphe_pack_squeeze",
+    "fphe_clock_stamp", "fphe_pack_squeeze", "fphe_positions_terms",
 )
 
 _lock = threading.Lock()
@@ -119,6 +119,10 @@ def load() -> ctypes.CDLL:
         lib.fphe_fold_segments.argtypes = [vp, vp, vp, vp, ctypes.c_size_t, vp, vp, ctypes.c_size_t, ctypes.c_size_t,
                                            vp, vp, vp, vp, vp, vp]
         lib.fphe_fold_segments.restype = st
+        if hasattr(lib, "fphe_positions_terms"):  # an A/B build from before it (FPHE_LIB_PATH) lacks it
+            lib.fphe_positions_terms.argtypes = [vp, ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int32,
+                                                 ctypes.c_size_t, vp, vp, vp]
+            lib.fphe_positions_terms.restype = st
         if hasattr(lib, "fphe_add_order"):  # an A/B build from before it (FPHE_LIB_PATH) lacks it
             lib.fphe_add_order.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_uint32, vp, vp]
             lib.fphe_add_order.restype = st

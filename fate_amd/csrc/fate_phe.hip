@@ -939,6 +939,26 @@ fphe_status launch_fold27(fphe_ctx* c, const uint32_t* Src, const uint8_t* ssign
   return hip_ok(hipGetLastError());
 }
 
+// ---- SecureBoost bin indexes -> fold terms (fphe_positions_terms) ---------------------------
+// positions [ns][npos] (int32 or int64, sample-major as iupdate's Vec<Vec<usize>>): term
+// (i, j, t) = pair p = i npos + j, then t < stride, at p stride + t: src = i stride + t, slot =
+// pos stride + t, or -1 when pos is outside [0, lim) (fphe_fold_segments then reports the
+// segment out of range).  One thread per pair; the range test runs on the position's own width.
+template <typename PT>
+__global__ __launch_bounds__(256) void k_positions_terms(const PT* __restrict__ pos, size_t npairs, uint32_t npos,
+                                                          int32_t stride, int64_t lim, int32_t* __restrict__ src,
+                                                          int32_t* __restrict__ slot) {
+  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < npairs; p += (size_t)gridDim.x * blockDim.x) {
+    const int64_t v = (int64_t)pos[p];
+    const bool ok = v >= 0 && v < lim;
+    const int32_t i = (int32_t)(p / npos);
+    for (int32_t t = 0; t < stride; ++t) {
+      src[p * stride + t] = i * stride + t;
+      slot[p * stride + t] = ok ? (int32_t)v * stride + t : -1;
+    }
+  }
+}
+
 // ---- segmented fold with device grouping (fphe_fold_segments) --------------------------------
 // Stream-ordered scratch of one call: freed (hipFreeAsync) on the call's stream at the end.
 // Small requests are carved from 64-MiB arenas (256-B aligned) and large ones get their own
@@ -2198,6 +2218,28 @@ fphe_status fphe_fold_segments(fphe_ctx* c, const uint32_t* Src, const uint8_t* 
                                   (hipStream_t)stream);
 }
 
+
+fphe_status fphe_positions_terms(const void* positions, int pos_i64, size_t ns, size_t npos, int32_t stride,
+                                 size_t nslots, int32_t* src, int32_t* slot, void* stream) {
+  if (stride < 1 || npos >= (1ull << 32)) return FPHE_ERR_ARG;
+  const size_t npairs = ns * npos;
+  if (npairs == 0) return FPHE_OK;
+  if (!positions || !src || !slot) return FPHE_ERR_ARG;
+  // every src and slot value fits int32 (fphe_fold_segments' widths): terms and samples
+  if (npairs > ((1ull << 31) - 1) / (size_t)stride || ns > ((1ull << 31) - 1) / (size_t)stride ||
+      nslots >= (1ull << 31))
+    return FPHE_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t lim = (int64_t)(nslots / (size_t)stride);
+  const unsigned grid = (unsigned)std::min<size_t>((npairs + 255) / 256, 4096);
+  if (pos_i64)
+    hipLaunchKernelGGL(k_positions_terms<int64_t>, dim3(grid), dim3(256), 0, s, (const int64_t*)positions, npairs,
+                       (uint32_t)npos, stride, lim, src, slot);
+  else
+    hipLaunchKernelGGL(k_positions_terms<int32_t>, dim3(grid), dim3(256), 0, s, (const int32_t*)positions, npairs,
+                       (uint32_t)npos, stride, lim, src, slot);
+  return hip_ok(hipGetLastError());
+}
 
 fphe_status fphe_decrypt(fphe_ctx* c, const uint32_t* C, size_t count, uint32_t* P, void* stream) {
   if (!c) return FPHE_ERR_ARG;

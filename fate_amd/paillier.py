@@ -870,15 +870,21 @@ class CiphertextVector:
             # straight from it, in the reference's sample-major order, in four launches
             # (sample i's ids are implied: only the positions need a range check)
             ns, npos = indexes.shape
-            pp = indexes.to(device=self.device).reshape(-1)
             st = max(int(stride), 1)
-            lo, hi = torch.stack(list(torch.aminmax(pp))).to(torch.int64).tolist()  # one read-back
-            if lo < 0 or (hi + 1) * st > self.count or ns * st > other.count:
+            if ns * st > other.count:
                 raise PanicException("index out of bounds")
-            t = torch.arange(st, device=self.device, dtype=torch.int32)
-            slot = torch.add(t, pp.to(torch.int32).view(-1, 1), alpha=st).reshape(-1)
-            base = torch.arange(ns, device=self.device, dtype=torch.int32).view(-1, 1, 1)
-            src = torch.add(t.view(1, 1, -1), base, alpha=st).expand(ns, npos, st).reshape(-1)
+            pp = indexes.to(device=self.device)
+            if pp.dtype not in (torch.int32, torch.int64):
+                pp = pp.to(torch.int64)
+            pp = pp.contiguous()
+            src = torch.empty(ns * npos * st, dtype=torch.int32, device=self.device)
+            slot = torch.empty_like(src)
+            # one launch, no read-back: a position out of [0, count / stride) becomes slot -1,
+            # which the fold reports (FPHE_ERR_ARG -> the reference's index panic)
+            _lib.check(_lib.load().fphe_positions_terms(_ptr(pp), int(pp.dtype == torch.int64), ns, npos, st,
+                                                        self.count, _ptr(src), _ptr(slot),
+                                                        ctypes.c_void_p(_stream(self.device))),
+                       "fphe_positions_terms")
             self._fold_terms(other, src, slot, pk)
             return
         ii, pp = _flatten_positions(indexes, self.device)

@@ -250,6 +250,17 @@ fphe_status fphe_fold_segments(fphe_ctx* ctx, const uint32_t* Src, const uint8_t
                                size_t nsrc, const int32_t* idx, const int32_t* seg, size_t nterms, size_t nseg,
                                uint32_t* Co, uint8_t* so, int32_t* eo, uint8_t* present, int32_t* err, void* stream);
 
+/* SecureBoost's bin indexes as fold terms: the term lists CiphertextVector::iupdate
+ * (fixedpoint_paillier/src/lib.rs:724-735; paillier.rs:261-270) walks for a [ns][npos]
+ * position matrix (int32, or int64 when pos_i64), sample-major: term (i, j, t), t < stride, at
+ * index (i npos + j) stride + t reads src = i stride + t into slot = pos[i][j] stride + t of an
+ * nslots-element histogram.  A position outside [0, nslots / stride) -- the reference's index
+ * panic -- gets slot -1, which fphe_fold_segments reports as FPHE_ERR_ARG.  Writes
+ * ns npos stride int32 entries to src and slot; no host sync.  FPHE_ERR_ARG when an index
+ * would not fit int32. */
+fphe_status fphe_positions_terms(const void* positions, int pos_i64, size_t ns, size_t npos, int32_t stride,
+                                 size_t nslots, int32_t* src, int32_t* slot, void* stream);
+
 /* Co = Ca^(2^nsq) * Cb mod n^2 with so = sb: the step of CiphertextVector::pack_squeeze
  * (paillier.rs:241-243; fixedpoint_paillier/src/lib.rs:439-450), `result.pow_mod_mut(2^shift)`
  * then `result * y % ns` (the powm result is canonical, so the product takes y's sign). */

@@ -209,9 +209,19 @@ def test_iupdate_position_range_checked_before_narrowing(env):
     fx, sk, pk, coder, opk, cts = env
     v = dev_vec(pk, more(opk, cts, 4))
     hist = P.CiphertextVector.zeros(4, pk._key.L2)
-    for bad in ([[0], [(1 << 32) + 1]], torch.tensor([[0], [(1 << 32) + 1]]), torch.tensor([[0], [-1]])):
+    for bad in ([[0], [(1 << 32) + 1]], torch.tensor([[0], [(1 << 32) + 1]]), torch.tensor([[0], [-1]]),
+                torch.tensor([[0], [4]], dtype=torch.int32), torch.tensor([[0], [-1]], dtype=torch.int32)):
         with pytest.raises(P.PanicException):
             hist.iupdate(v, bad, 1, pk)
+    # stride 3 over 4 slots: position 1 reaches slots 3, 4, 5 -- past the end, as the reference's
+    # index panic (fphe_positions_terms: positions below count / stride only)
+    with pytest.raises(P.PanicException):
+        hist.iupdate(v, torch.tensor([[1]], dtype=torch.int32), 3, pk)
+    # a valid uint8 position matrix takes the same path (widened) and equals the list form
+    a, b = P.CiphertextVector.zeros(4, pk._key.L2), P.CiphertextVector.zeros(4, pk._key.L2)
+    a.iupdate(v, torch.tensor([[3, 0], [1, 1]], dtype=torch.uint8), 1, pk)
+    b.iupdate(v, [[3, 0], [1, 1]], 1, pk)
+    assert host(pk, a) == host(pk, b)
 
 
 def test_fold_raised_keys_forced(env, monkeypatch):
