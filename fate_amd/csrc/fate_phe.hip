@@ -63,8 +63,11 @@ constexpr int kWinSlide = 6;     // sliding window of the 27-bit engine's shared
 #ifndef FPHE_WIN_DEC1
 #define FPHE_WIN_DEC1 5
 #endif
+#ifndef FPHE_WIN_DEC2
+#define FPHE_WIN_DEC2 6
+#endif
 template <int TPI>
-constexpr int kWinDec = TPI == 1 ? FPHE_WIN_DEC1 : kWinSlide;
+constexpr int kWinDec = TPI == 1 ? FPHE_WIN_DEC1 : (TPI == 2 ? FPHE_WIN_DEC2 : kWinSlide);
 constexpr int kWinMul = 4;       // window of the per-lane-exponent modexp (ct x pt): table capacity
 #ifndef FPHE_MUL_ADAPT
 #define FPHE_MUL_ADAPT 1  // ct x pt: 3-bit window for short exponents, all-zero windows skipped
