@@ -330,6 +330,19 @@ def test_other_key_sizes_bit_exact(bits):
     sq = c.pack_squeeze(3, 61, pk)
     osq = O.pack_squeeze(opk, oc, 3, 61)
     assert sq.to_signed_ints(pk.ns) == ([t.c for t in osq], [t.exp for t in osq])
+    # the key holder's device-drawn obfuscation ((z_p, z_q), k_draw_z) at this geometry: few
+    # elements (k_pow_half_enc_wide) and past the latency threshold (k_pow_half27<., ., true,
+    # true>) decrypt to the inputs, and the obfuscation is an n-th residue (x^lambda = 1 mod n^2)
+    lam = (sk.p - 1) * (sk.q - 1)
+    kd = pk.encrypt_encoded(pv, True)
+    assert coder.decode_f64_vec(sk.decrypt_to_encoded(kd)).cpu().tolist() == xs
+    cs, _ = kd.to_signed_ints(pk.ns)
+    for cc, s_ in list(zip(cs, sig))[:3]:
+        xo = (cc % pk.ns) * pow((1 + (s_ % pk.n) * pk.n) % pk.ns, -1, pk.ns) % pk.ns
+        assert pow(xo, lam, pk.ns) == 1
+    xb = torch.randn(4100, generator=torch.Generator().manual_seed(bits), dtype=torch.float64, device="cpu").cuda()
+    kb = pk.encrypt_encoded(coder.encode_f64_vec(xb), True)
+    assert torch.equal(coder.decode_f64_vec(sk.decrypt_to_encoded(kb)), xb)
 
 
 def test_unsupported_key_sizes_decline():
