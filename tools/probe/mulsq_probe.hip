@@ -1,4 +1,5 @@
-// Throughput probe of the 28-bit engine at TPI 4 (2048-bit keys' n^2, 148 limbs): what a wave
+// Throughput probe of the 28-bit engine at TPI 4 (2048-bit keys' n^2, 148 limbs; -DPROBE_TPI=2:
+// p^2 / q^2 of 2048-bit keys, 74 limbs, the sq and mul modes only): what a wave
 // sustains per element for
 //   sq      : sqr() chains (the encrypt kernel's bulk)
 //   mul     : mont_mul() with a fixed operand already in the LDS slot
@@ -15,7 +16,10 @@
 using namespace fphe;
 using namespace fphe::r28;
 
-constexpr int TPI = 4;
+#ifndef PROBE_TPI
+#define PROBE_TPI 4
+#endif
+constexpr int TPI = PROBE_TPI;
 using G = Geo<TPI>;
 constexpr int E = G::E, NL = G::NL;
 
@@ -170,6 +174,7 @@ int main(int argc, char** argv) {
   run<1, 3>("mul", dN, np, io, rows, nrows, cus, iters);
   run<2, 2>("mulslot", dN, np, io, rows, nrows, cus, iters);
   run<2, 3>("mulslot", dN, np, io, rows, nrows, cus, iters);
+  if (TPI != 4) return 0;  // the fold modes gather 128-word rows
   run<3, 2>("fold", dN, np, io, rows, nrows, cus, iters);
   run<3, 3>("fold", dN, np, io, rows, nrows, cus, iters);
   run<4, 2>("foldrnd", dN, np, io, rows, nrows, cus, iters);
