@@ -16,7 +16,7 @@ import ctypes
 import itertools
 import os
 import threading
-from typing import Dict, List, Optional, Sequence, Tuple, Union
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
