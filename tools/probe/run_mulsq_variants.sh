@@ -3,9 +3,10 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
+OUT=${OUT:-gpurun_out/mulsq_variants.txt}
 for v in "$@"; do
-  echo "== $v" >> gpurun_out/r05ac_probe.txt
+  echo "== $v" >> $OUT
   it=400; case $v in t2*) it=800;; esac
-  timeout -k 10 120 tools/probe/mulsq_$v $it 1 >> gpurun_out/r05ac_probe.txt 2>&1 || exit 1
+  timeout -k 10 120 tools/probe/mulsq_$v $it 1 >> $OUT 2>&1 || exit 1
 done
-grep -E "==|^sq|^mul " gpurun_out/r05ac_probe.txt
+grep -E "==|^sq|^mul " $OUT
