@@ -225,6 +225,42 @@ def test_two_streams_share_a_context(k1024):
         assert torch.equal(y.cpu().view(torch.int32), x.cpu().view(torch.int32))
 
 
+def test_two_threads_share_a_context(k1024):
+    """Two host threads, each on its own HIP stream, run encrypt -> ct-add -> ct x pt ->
+    decrypt loops with one key context at once (the context's lock orders the launches and
+    its scratch hand-over between streams): every result decodes to the float64 value of the
+    same ops."""
+    import threading
+    p, q, sk, pk, coder, osk, opk = k1024
+    errors = []
+
+    def work(seed, n):
+        try:
+            g = torch.Generator().manual_seed(seed)
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                for _ in range(3):
+                    x = torch.randint(-1000, 1000, (n,), generator=g).double().cuda()
+                    y = torch.randint(-1000, 1000, (n,), generator=g).double().cuda()
+                    w = torch.randint(-9, 9, (n,), generator=g).double().cuda()
+                    cx = pk.encrypt_encoded(coder.encode_f64_vec(x), True)
+                    cy = pk.encrypt_encoded(coder.encode_f64_vec(y), True)
+                    r = cx.add(pk, cy).mul(pk, coder.encode_f64_vec(w))
+                    got = coder.decode_f64_vec(sk.decrypt_to_encoded(r))
+                    s.synchronize()
+                    if not torch.equal(got, (x + y) * w):
+                        errors.append(seed)
+        except Exception as e:  # surfaced below
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=work, args=(seed, n)) for seed, n in ((1, 300), (2, 5000))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors
+
+
 @pytest.mark.parametrize("bits,seed", [(1024, 0), (1024, 1), (1024, 2), (2048, 0), (2048, 1)])
 def test_random_op_chains_vs_oracle(bits, seed):
     """Randomised chains of the element-wise ops (add / sub / rsub / add_pt / ct x pt with
