@@ -26,3 +26,25 @@ def test_rank_command_line():
     assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1" and "--master-port=29511" in cmd
     tail = cmd[cmd.index(os.path.abspath(bench.__file__)) + 1:]
     assert tail == ["--gpus", "4", "--elements", "4096", "--steps=3", "--elements=64", "--total", "100"]
+
+
+def test_keyholder_credit_follows_the_draw(monkeypatch):
+    """rooflines' key-holder credit (bench.enc_crt_mac32_per_elem) counts the modexps that run:
+    with the (z_p, z_q) draw one |p|-bit exponent mod s^2 per half, else the split (keys above
+    1024 bits: an extra |p|-bit exponent mod s) or one |n|-bit exponent mod s^2; and
+    bench.kh_direct_z mirrors the library's switch (FPHE_KH_DIRECT_Z, gcd(q, p-1) =
+    gcd(p, q-1) = 1)."""
+    import bench
+    for bits in (1024, 2048, 4096):
+        d, r = bench.enc_crt_mac32_per_elem(bits, True), bench.enc_crt_mac32_per_elem(bits, False)
+        assert 0 < d < r
+    # 2048 bits: per half (1024 + 205 + 16) products over the 64-word p^2 against two such
+    # exponents (mod p, then mod p^2): the direct draw saves the first step only
+    rec = 4 * bench.mac32_per_mont(128)
+    assert bench.enc_crt_mac32_per_elem(2048, True) == 2 * 1245 * bench.mac32_per_mont(64) + rec
+    p, q = 1019, 1031  # q does not divide p - 1, p does not divide q - 1
+    monkeypatch.delenv("FPHE_KH_DIRECT_Z", raising=False)
+    assert bench.kh_direct_z(p, q)
+    assert not bench.kh_direct_z(11, 23)  # 11 | 23 - 1
+    monkeypatch.setenv("FPHE_KH_DIRECT_Z", "0")
+    assert not bench.kh_direct_z(p, q)
