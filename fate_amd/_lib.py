@@ -30,9 +30,16 @@ EF_NOT_INVERTIBLE = 0x10
 EF_DECODE_I128 = 0x20
 EF_EXP_RANGE = 0x40
 
+# fphe_ctx_set_option / fphe_ctx_get_option (include/fate_phe.h)
+OPT_WIDE_DECRYPT_MAX = 1
+OPT_WIDE_ENCRYPT_MAX = 2
+OPT_WIDE_KH_ENCRYPT_MAX = 3
+OPT_KH_DIRECT_Z = 4
+
 # every symbol declared in include/fate_phe.h
 EXPORTED_SYMBOLS = (
     "fphe_ctx_create", "fphe_ctx_destroy", "fphe_ctx_limbs", "fphe_ctx_mont_one",
+    "fphe_ctx_set_option", "fphe_ctx_get_option",
     "fphe_encode_f32", "fphe_encode_f64", "fphe_decode_f32", "fphe_decode_f64",
     "fphe_encode_i64", "fphe_decode_i64", "fphe_decode_i32", "fphe_pack_f64", "fphe_unpack_f64",
     "fphe_encrypt", "fphe_encrypt_crt", "fphe_decrypt", "fphe_add", "fphe_add_ordered", "fphe_add_order", "fphe_mul", "fphe_neg", "fphe_sqmul", "fphe_align",
@@ -72,6 +79,11 @@ def load() -> ctypes.CDLL:
         if hasattr(lib, "fphe_ctx_mont_one"):  # an A/B build from before it (FPHE_LIB_PATH) lacks it
             lib.fphe_ctx_mont_one.argtypes = [vp, c_u32p]
             lib.fphe_ctx_mont_one.restype = st
+        if hasattr(lib, "fphe_ctx_set_option"):  # an A/B build from before it (FPHE_LIB_PATH) lacks it
+            lib.fphe_ctx_set_option.argtypes = [vp, ctypes.c_int, ctypes.c_int64]
+            lib.fphe_ctx_set_option.restype = st
+            lib.fphe_ctx_get_option.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]
+            lib.fphe_ctx_get_option.restype = st
         for name in ("fphe_encode_f32", "fphe_encode_f64"):
             f = getattr(lib, name)
             f.argtypes = [vp, vp, ctypes.c_size_t, vp, vp, vp, vp, vp]

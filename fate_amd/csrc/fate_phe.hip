@@ -25,36 +25,18 @@ namespace {
 
 constexpr int kBlock = 256;      // 4 waves per workgroup
 constexpr int kWavesPerBlock = kBlock / FPHE_WAVE;
-// decryptions of at most this many elements run their half-size modexps on the one-element-
-// per-wave latency kernel (wide_dev.h k_pow_half_wide): the throughput kernel takes ~25 ms for
-// anything up to ~32k elements (its waves run alone at their per-row latency), the latency
-// kernel 4.3 ms for up to ~300 and 10.9 ms for 2,048 (profiles/r05/r05g_latency_leg.txt)
-// (env FPHE_WIDE_DECRYPT_MAX overrides, read once: 0 turns the path off, for A/B and tests)
-inline size_t env_size(const char* name, size_t dflt) {
+// Path selection per context (fphe_ctx_set_option, include/fate_phe.h): calls of at most
+// this many elements run the one-element-per-wave latency kernels (wide_dev.h).  Decrypt: the
+// throughput kernel takes ~25 ms for anything up to ~32k elements (its waves run alone at their
+// per-row latency), the latency kernel 4.3 ms for up to ~300 and 10.9 ms for 2,048
+// (profiles/r05/r05g_latency_leg.txt).  Public-key encrypt: the throughput kernel takes ~52 ms
+// up to ~16k elements.  Key-holder encrypt with drawn (z_p, z_q): the z^s mod s^2 halves on
+// k_pow_half_enc_wide (decrypt's chain shape).  The env variables set a new context's
+// defaults (0 turns a latency path off); tests switch them per context to run the parity
+// fixtures through both kernels of each op.
+inline int64_t env_i64(const char* name, int64_t dflt) {
   const char* e = getenv(name);
-  return e ? (size_t)strtoull(e, nullptr, 10) : dflt;
-}
-inline size_t wide_decrypt_max() {
-  static const size_t v = env_size("FPHE_WIDE_DECRYPT_MAX", 4096);
-  return v;
-}
-// the key holder's device-drawn obfuscation in CRT coordinates (k_draw_z); FPHE_KH_DIRECT_Z=0:
-// r and the two-step modexp as for injected r (A/B)
-inline bool kh_direct_z() {
-  static const bool v = env_size("FPHE_KH_DIRECT_Z", 1) != 0;
-  return v;
-}
-// key-holder encryptions with drawn (z_p, z_q) of at most this many elements run their
-// z^s mod s^2 halves on the latency kernel (k_pow_half_enc_wide, decrypt's chain shape)
-inline size_t wide_kh_encrypt_max() {
-  static const size_t v = env_size("FPHE_WIDE_KH_ENCRYPT_MAX", 4096);
-  return v;
-}
-// obfuscated public-key encryptions of at most this many elements likewise (k_encrypt_wide):
-// the throughput kernel takes ~52 ms for anything up to ~16k elements (FPHE_WIDE_ENCRYPT_MAX)
-inline size_t wide_encrypt_max() {
-  static const size_t v = env_size("FPHE_WIDE_ENCRYPT_MAX", 2048);
-  return v;
+  return e ? (int64_t)strtoll(e, nullptr, 10) : dflt;
 }
 constexpr int kWinSlide = 6;     // sliding window of the 27-bit engine's shared-exponent modexps
 // the decrypt halves of <= 1024-bit keys (TPI 1, exponents p-1 / q-1 of <= 512 bits): a 5-bit
@@ -285,12 +267,15 @@ __global__ __launch_bounds__(256) void k_draw_r(KeyArgs K, size_t count, ChaChaK
 // n^2 with the distribution of the reference's random_rn (paillier/src/lib.rs:94-98;
 // random.rs:22-25, r in [1, n-1]: the r sharing a factor with n, probability < 2^-1000, aside)
 // for the cost of the second step only.  Injected r (parity mode) keeps the two-step path.
-// z_s uniform in [1, s-1] from element e's ChaCha20 stream of half h (nonce tweaked per half,
-// so the streams are disjoint from each other and from draw_r's); rows of Z as k_pow_small27
-// writes them.
+// z_s uniform in [1, s-1] from element e's ChaCha20 stream of half h.  The call's nonce is
+// used as is; the streams are told apart in the block counter: bit 31 set for (z_p, z_q), clear
+// for draw_r, bit 30 = h.  The low 16 bits count blocks (attempt NB + b, far below 2^14 in
+// practice: each attempt succeeds with probability > 1/2) and bits 16..29 carry e >> 32 (0:
+// a call has fewer than 2^32 elements), so no two draws of one call share a ChaCha20 block.
+constexpr u32 kDrawZTag = 1u << 31, kDrawHalfTag = 1u << 30;
 template <int LQ>
 __device__ __forceinline__ void draw_below(u32 (&A)[LQ], const u32* __restrict__ sm1, int sbits, const ChaChaKey& ck,
-                                           u64 nonce, size_t e) {
+                                           u64 nonce, size_t e, u32 tag) {
   constexpr int NB = (LQ + 15) / 16;
   auto wmask = [&](int j) -> u32 {
     const int b = sbits - 32 * j;
@@ -304,8 +289,8 @@ __device__ __forceinline__ void draw_below(u32 (&A)[LQ], const u32* __restrict__
 #pragma unroll
       for (int b = 0; b < NB; ++b) {
         u32 blk[16];
-        chacha20_block(ck, (attempt * NB + b) | ((u32)(e >> 32) << 16), (u32)e, (u32)(nonce >> 32), (u32)nonce,
-                       blk);
+        chacha20_block(ck, (attempt * NB + b) | ((u32)(e >> 32) << 16) | tag, (u32)e, (u32)(nonce >> 32),
+                       (u32)nonce, blk);
 #pragma unroll
         for (int i = 0; i < 16; ++i)
           if (b * 16 + i < LQ) x[b * 16 + i] = blk[i];
@@ -342,8 +327,8 @@ __global__ __launch_bounds__(256) void k_draw_z(KeyArgs K, size_t count, ChaChaK
 #pragma unroll 1
     for (u32 h = 0; h < 2; ++h) {
       u32 z[LQ];
-      draw_below<LQ>(z, h ? K.qm1 : K.pm1, h ? K.q_bits : K.p_bits, ck,
-                     nonce ^ (0x9E3779B97F4A7C15ull * (h + 1)), ebase + e);
+      draw_below<LQ>(z, h ? K.qm1 : K.pm1, h ? K.q_bits : K.p_bits, ck, nonce, ebase + e,
+                     kDrawZTag | (h ? kDrawHalfTag : 0u));
 #pragma unroll
       for (u32 j = 0; j < ZW; ++j) Z[tiled(e, 2 * ZW, h * ZW + j)] = j < (u32)LQ ? z[j] : 0u;
     }
@@ -649,6 +634,10 @@ struct fphe_ctx {
   // the key holder may draw its obfuscation as (z_p, z_q) directly (k_draw_z): set when
   // gcd(q, p - 1) = gcd(p, q - 1) = 1, which makes r -> (z_p, z_q) a bijection
   bool kh_direct = false;
+  // path options (fphe_ctx_set_option): latency-kernel thresholds, and whether the key holder
+  // draws (z_p, z_q) (effective only when kh_direct)
+  int64_t wide_decrypt_max = 4096, wide_encrypt_max = 2048, wide_kh_encrypt_max = 4096;
+  bool kh_direct_z = true;
   std::mutex mu;
 };
 
@@ -662,6 +651,20 @@ struct DevGuard {
   int prev = 0;
   explicit DevGuard(int d) { (void)hipGetDevice(&prev); (void)hipSetDevice(d); }
   ~DevGuard() { (void)hipSetDevice(prev); }
+};
+
+// context-less entry points launch on the device of the caller's stream (a non-null stream;
+// on the null stream, on the current device, which the caller sets)
+struct StreamDevGuard {
+  int prev = -1;
+  explicit StreamDevGuard(void* stream) {
+    hipDevice_t d;
+    if (stream && hipStreamGetDevice((hipStream_t)stream, &d) == hipSuccess && hipGetDevice(&prev) == hipSuccess)
+      (void)hipSetDevice(d);
+    else
+      prev = -1;
+  }
+  ~StreamDevGuard() { if (prev >= 0) (void)hipSetDevice(prev); }
 };
 
 Limbs from_words(const uint32_t* w, size_t n) { return hbn::norm(Limbs(w, w + n)); }
@@ -774,7 +777,7 @@ fphe_status launch_encrypt27(fphe_ctx* c, const uint32_t* P, uint32_t lp, const 
   ChaChaKey ck;
   if (draw)
     for (int i = 0; i < 8; ++i) ck.k[i] = key[i];
-  if (obf && count <= wide_encrypt_max()) {
+  if (obf && (int64_t)count <= c->wide_encrypt_max) {
     // few elements: one wave per element on the latency kernel (wide_dev.h), M-form written
     // directly; r drawn as on the throughput path (element e's stream), so the integers agree
     const size_t rb = (size_t)ntiles_of(count) * L1 * FPHE_WAVE * 4;
@@ -811,7 +814,7 @@ fphe_status launch_encrypt27(fphe_ctx* c, const uint32_t* P, uint32_t lp, const 
 template <int L>
 fphe_status launch_decrypt27(fphe_ctx* c, const uint32_t* C, size_t count, uint32_t* P, hipStream_t s) {
   constexpr int TPI = L / 64, E = FPHE_WAVE / TPI, NL = rad_ll(TPI) * TPI, LH = L / 2, LQ = L / 4;
-  if (count <= wide_decrypt_max()) {
+  if ((int64_t)count <= c->wide_decrypt_max) {
     // few elements: one wave per (element, half) on the latency kernel (wide_dev.h), which
     // writes the same y_s rows k_pow_half27 does; the CRT tail is the same kernel
     const size_t ybytes = (size_t)ntiles_of(count) * 2 * LH * FPHE_WAVE * 4;
@@ -871,8 +874,8 @@ fphe_status launch_encrypt_crt27(fphe_ctx* c, const uint32_t* P, uint32_t lp, co
   const size_t lds0 = (size_t)kWavesPerBlock * NLs * Es * 4;
   unsigned g0 = 0;
   size_t zbytes = 0;
-  const bool direct = !r && c->kh_direct && kh_direct_z();
-  if (kKhSplit<L>) {
+  const bool direct = !r && c->kh_direct && c->kh_direct_z;
+  if (kKhSplit<L> && !direct) {  // the direct draw skips the first step (and its table)
     set_lds(k0, lds0);
     g0 = occ_grid(c, k0, lds0, (m0 + Es - 1) / Es, "pow_small27");
     tbytes = std::max(tbytes, (size_t)g0 * kWavesPerBlock * kTabEntries<kWinSlide> * rad_ll(TPIs) * FPHE_WAVE * 4);
@@ -884,7 +887,7 @@ fphe_status launch_encrypt_crt27(fphe_ctx* c, const uint32_t* P, uint32_t lp, co
   if (direct && !kKhSplit<L>) set_lds(k1z, lds1);
   const size_t ybytes = (size_t)ntiles_of(m0) * 2 * L1 * FPHE_WAVE * 4;
   const size_t rbytes = (size_t)ntiles_of(m0) * L1 * FPHE_WAVE * 4;
-  if (ensure_scratch(c, tbytes + ybytes + zbytes + (r ? 0 : rbytes), s) != FPHE_OK) return FPHE_ERR_HIP;
+  if (ensure_scratch(c, tbytes + ybytes + zbytes + ((r || direct) ? 0 : rbytes), s) != FPHE_OK) return FPHE_ERR_HIP;
   u32* Y = c->scratch + tbytes / 4;
   u32* Z = Y + ybytes / 4;
   ChaChaKey ck;
@@ -900,7 +903,7 @@ fphe_status launch_encrypt_crt27(fphe_ctx* c, const uint32_t* P, uint32_t lp, co
     const unsigned rgrid = (unsigned)std::min<size_t>((m + 255) / 256, (size_t)c->cus * 4);
     if (direct) {  // (z_p, z_q) drawn in place of r and its first modexp step
       hipLaunchKernelGGL(k_draw_z<L>, dim3(rgrid), dim3(256), 0, s, c->K, m, ck, nonce, e0, Z);
-      if (count <= wide_kh_encrypt_max())  // few elements: one per wave and half
+      if ((int64_t)count <= c->wide_kh_encrypt_max)  // few elements: one per wave and half
         hipLaunchKernelGGL((k_pow_half_enc_wide<L, kWinDec<TPIh>>), dim3((unsigned)(2 * m)), dim3(64), 0, s, c->K,
                            (const u32*)Z, m, Y);
       else
@@ -1926,6 +1929,10 @@ fphe_status fphe_ctx_create(int device, uint32_t key_bits, const uint32_t* n_w, 
     auto* c = new fphe_ctx();
     c->device = device; c->key_bits = key_bits; c->L1 = L1; c->L2 = L2; c->LQ = LQ; c->has_sk = has_sk;
     c->kh_direct = has_sk && kh_direct;
+    c->wide_decrypt_max = env_i64("FPHE_WIDE_DECRYPT_MAX", 4096);
+    c->wide_encrypt_max = env_i64("FPHE_WIDE_ENCRYPT_MAX", 2048);
+    c->wide_kh_encrypt_max = env_i64("FPHE_WIDE_KH_ENCRYPT_MAX", 4096);
+    c->kh_direct_z = env_i64("FPHE_KH_DIRECT_Z", 1) != 0;
     DevGuard g(device);
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) { delete c; return FPHE_ERR_HIP; }
@@ -1995,6 +2002,30 @@ fphe_status fphe_ctx_destroy(fphe_ctx* c) {
   }
   delete c;
   return FPHE_OK;
+}
+
+fphe_status fphe_ctx_set_option(fphe_ctx* c, int option, int64_t value) {
+  if (!c) return FPHE_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);  // not while a call of this context is being queued
+  switch (option) {
+    case FPHE_OPT_WIDE_DECRYPT_MAX: c->wide_decrypt_max = value; return FPHE_OK;
+    case FPHE_OPT_WIDE_ENCRYPT_MAX: c->wide_encrypt_max = value; return FPHE_OK;
+    case FPHE_OPT_WIDE_KH_ENCRYPT_MAX: c->wide_kh_encrypt_max = value; return FPHE_OK;
+    case FPHE_OPT_KH_DIRECT_Z: c->kh_direct_z = value != 0; return FPHE_OK;
+    default: return FPHE_ERR_ARG;
+  }
+}
+
+fphe_status fphe_ctx_get_option(fphe_ctx* c, int option, int64_t* value) {
+  if (!c || !value) return FPHE_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  switch (option) {
+    case FPHE_OPT_WIDE_DECRYPT_MAX: *value = c->wide_decrypt_max; return FPHE_OK;
+    case FPHE_OPT_WIDE_ENCRYPT_MAX: *value = c->wide_encrypt_max; return FPHE_OK;
+    case FPHE_OPT_WIDE_KH_ENCRYPT_MAX: *value = c->wide_kh_encrypt_max; return FPHE_OK;
+    case FPHE_OPT_KH_DIRECT_Z: *value = (c->kh_direct && c->kh_direct_z) ? 1 : 0; return FPHE_OK;
+    default: return FPHE_ERR_ARG;
+  }
 }
 
 fphe_status fphe_ctx_limbs(const fphe_ctx* c, uint32_t* l2, uint32_t* l1) {
@@ -2224,6 +2255,7 @@ fphe_status fphe_fold_segments(fphe_ctx* c, const uint32_t* Src, const uint8_t* 
 
 fphe_status fphe_positions_terms(const void* positions, int pos_i64, size_t ns, size_t npos, int32_t stride,
                                  size_t nslots, int32_t* src, int32_t* slot, void* stream) {
+  StreamDevGuard sdg(stream);
   if (stride < 1 || npos >= (1ull << 32)) return FPHE_ERR_ARG;
   const size_t npairs = ns * npos;
   if (npairs == 0) return FPHE_OK;
@@ -2275,6 +2307,7 @@ fphe_status fphe_add_ordered(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa,
 
 fphe_status fphe_add_order(const int32_t* ea, const int32_t* eb, size_t count, uint32_t L2, int32_t* order,
                            void* stream) {
+  StreamDevGuard sdg(stream);
   if (count == 0) return FPHE_OK;
   if (!ea || !eb || !order || (L2 != 64 && L2 != 128 && L2 != 256)) return FPHE_ERR_ARG;
   if (count >= (1ull << 31)) return FPHE_ERR_ARG;
@@ -2396,6 +2429,7 @@ fphe_status fphe_mul(fphe_ctx* c, const uint32_t* Ca, const uint8_t* sa, const i
 
 fphe_status fphe_chacha20_blocks(const uint32_t key[8], uint32_t counter, const uint32_t nonce[3], size_t nblocks,
                                  uint32_t* out, void* stream) {
+  StreamDevGuard sdg(stream);
   if (!key || !nonce || (nblocks && !out)) return FPHE_ERR_ARG;
   if (nblocks == 0) return FPHE_OK;
   ChaChaKey ck;
@@ -2409,6 +2443,7 @@ fphe_status fphe_chacha20_blocks(const uint32_t key[8], uint32_t counter, const 
 fphe_status fphe_permute(const uint32_t* Cin, const uint8_t* sin, const int32_t* ein, uint32_t L,
                          const int64_t* idx, size_t count, size_t nspace, int scatter, uint32_t* Cout,
                          uint8_t* sout, int32_t* eout, void* stream) {
+  StreamDevGuard sdg(stream);
   if (count == 0) return FPHE_OK;
   if (!idx || L == 0 || (Cin && !Cout) || (sin && !sout) || (ein && !eout)) return FPHE_ERR_ARG;
   const size_t words = ((count + FPHE_WAVE - 1) / FPHE_WAVE) * (size_t)L * FPHE_WAVE;
@@ -2479,6 +2514,7 @@ fphe_status fphe_ctx_mont_one(const fphe_ctx* c, uint32_t* one) {
 // ---- (8) wire format (see k_wire_encode) ----------------------------------------------
 fphe_status fphe_wire_lengths(const uint32_t* mag, const uint8_t* neg, uint32_t L, size_t count, int64_t* rec_len,
                               uint8_t* radix, void* stream) {
+  StreamDevGuard sdg(stream);
   if (count == 0) return FPHE_OK;
   if (!mag || !neg || !rec_len || !radix || L == 0) return FPHE_ERR_ARG;
   hipLaunchKernelGGL(k_wire_lengths, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, (hipStream_t)stream, mag,
@@ -2489,6 +2525,7 @@ fphe_status fphe_wire_lengths(const uint32_t* mag, const uint8_t* neg, uint32_t 
 fphe_status fphe_wire_encode(const uint32_t* mag, const uint8_t* neg, const int32_t* exp, uint32_t L, size_t count,
                              const int64_t* rec_off, const int64_t* rec_len, const uint8_t* radix, uint8_t* out,
                              void* stream) {
+  StreamDevGuard sdg(stream);
   if (count == 0) return FPHE_OK;
   if (!mag || !neg || !exp || !rec_off || !rec_len || !radix || !out || L == 0) return FPHE_ERR_ARG;
   const size_t threads = count * L;
@@ -2535,6 +2572,7 @@ fphe_status fphe_wire_scan(const uint8_t* buf, size_t nbytes, size_t pos, size_t
 
 fphe_status fphe_wire_decode(const uint8_t* buf, const int64_t* dig_off, const int32_t* dig_len, const int32_t* radix,
                              uint32_t L, size_t count, uint32_t* mag, int32_t* err, void* stream) {
+  StreamDevGuard sdg(stream);
   if (count == 0) return FPHE_OK;
   if (!buf || !dig_off || !dig_len || !radix || !mag || !err || L == 0) return FPHE_ERR_ARG;
   const size_t threads = count * L;
@@ -2562,6 +2600,7 @@ __global__ __launch_bounds__(64) void k_clock_stamp(unsigned long long* __restri
 }
 
 fphe_status fphe_clock_stamp(uint64_t* out, uint32_t blocks, uint32_t* wall_khz, void* stream) {
+  StreamDevGuard sdg(stream);
   if (!out || blocks == 0 || blocks > 65536) return FPHE_ERR_ARG;
   if (wall_khz) {
     int dev = 0, khz = 0;

@@ -184,14 +184,17 @@ def ciphertext_vector_records(cv: CiphertextVector, pk: Optional[PK] = None) -> 
     s = ctypes.c_void_p(_stream(dev))
     rec_len = torch.empty(n, dtype=torch.int64, device=dev)
     radix = torch.empty(n, dtype=torch.uint8, device=dev)
-    _lib.check(lib.fphe_wire_lengths(_ptr(mag), _ptr(neg), L, n, _ptr(rec_len), _ptr(radix), s), "fphe_wire_lengths")
+    with torch.cuda.device(dev):  # context-less entry points launch on the current device
+        _lib.check(lib.fphe_wire_lengths(_ptr(mag), _ptr(neg), L, n, _ptr(rec_len), _ptr(radix), s),
+                   "fphe_wire_lengths")
     ends = torch.cumsum(rec_len, 0)
     total = int(ends[-1].item())
     rec_off = ends - rec_len
     out = torch.empty(total, dtype=torch.uint8, device=dev)
     exp = exp.to(torch.int32).contiguous()
-    _lib.check(lib.fphe_wire_encode(_ptr(mag), _ptr(neg), _ptr(exp), L, n, _ptr(rec_off), _ptr(rec_len), _ptr(radix),
-                                    _ptr(out), s), "fphe_wire_encode")
+    with torch.cuda.device(dev):
+        _lib.check(lib.fphe_wire_encode(_ptr(mag), _ptr(neg), _ptr(exp), L, n, _ptr(rec_off), _ptr(rec_len),
+                                        _ptr(radix), _ptr(out), s), "fphe_wire_encode")
     return head, out
 
 
@@ -263,8 +266,9 @@ def ciphertext_vector_from_bincode(buf: bytes, pk: Optional[PK] = None, device=N
         d_off = torch.from_numpy(dig_off).to(dev)  # held until the launch is queued
         d_len = torch.from_numpy(dig_len).to(dev)
         d_rdx = torch.from_numpy(radix).to(dev)
-        _lib.check(lib.fphe_wire_decode(_ptr(dbuf), _ptr(d_off), _ptr(d_len), _ptr(d_rdx), L, n, _ptr(mag), _ptr(err),
-                                        s), "fphe_wire_decode")
+        with torch.cuda.device(dev):  # context-less: launches on the current device
+            _lib.check(lib.fphe_wire_decode(_ptr(dbuf), _ptr(d_off), _ptr(d_len), _ptr(d_rdx), L, n, _ptr(mag),
+                                            _ptr(err), s), "fphe_wire_decode")
     else:
         words = np.zeros((n, L), dtype=np.uint32)
         for e in range(n):

@@ -34,7 +34,10 @@
  *    neg uint8 [T*64] (1 = negative significand), exp int32 [T*64].
  *  - `stream` is a hipStream_t (NULL = default stream).  Calls are asynchronous
  *    on that stream; per-element error flags land in a device int32 word that the
- *    caller reads after synchronising.
+ *    caller reads after synchronising.  Calls with a context run on the context's device;
+ *    context-less calls (fphe_permute, fphe_add_order, fphe_positions_terms, fphe_wire_*,
+ *    fphe_chacha20_blocks, fphe_clock_stamp) on the device of a non-NULL `stream`, and on the
+ *    calling thread's current device for NULL.
  *  - Every function returns an fphe_status.
  */
 #ifndef FATE_PHE_H
@@ -86,6 +89,28 @@ fphe_status fphe_ctx_limbs(const fphe_ctx* ctx, uint32_t* l2, uint32_t* l1);
 /* M(1) = R mod n^2, the stored form of the literal 1 (Ciphertext::zero,
  * fixedpoint_paillier/src/lib.rs:244-249): L2 little-endian words into HOST memory. */
 fphe_status fphe_ctx_mont_one(const fphe_ctx* ctx, uint32_t* one);
+
+/* Path options of a context (not part of the reference's surface: which of two kernels with
+ * the same integer results runs a call).  Small calls run one element per wave on latency
+ * kernels; larger ones run the throughput kernels the bench times.
+ *   FPHE_OPT_WIDE_DECRYPT_MAX    fphe_decrypt of at most this many elements: latency kernel
+ *                                (default 4096, env FPHE_WIDE_DECRYPT_MAX; 0 = never)
+ *   FPHE_OPT_WIDE_ENCRYPT_MAX    obfuscated fphe_encrypt likewise (default 2048)
+ *   FPHE_OPT_WIDE_KH_ENCRYPT_MAX fphe_encrypt_crt with drawn (z_p, z_q) likewise (default 4096)
+ *   FPHE_OPT_KH_DIRECT_Z         1: fphe_encrypt_crt with r == NULL draws (z_p, z_q); 0: draws
+ *                                r and runs the two-step modexp (default 1, env
+ *                                FPHE_KH_DIRECT_Z).  get returns the effective value: 0 on a
+ *                                key where the direct draw is not a bijection.
+ * The env variables set a new context's defaults.  Setting waits for the context's lock, so
+ * it never changes a call being queued.  FPHE_ERR_ARG for an unknown option. */
+enum {
+  FPHE_OPT_WIDE_DECRYPT_MAX = 1,
+  FPHE_OPT_WIDE_ENCRYPT_MAX = 2,
+  FPHE_OPT_WIDE_KH_ENCRYPT_MAX = 3,
+  FPHE_OPT_KH_DIRECT_Z = 4,
+};
+fphe_status fphe_ctx_set_option(fphe_ctx* ctx, int option, int64_t value);
+fphe_status fphe_ctx_get_option(fphe_ctx* ctx, int option, int64_t* value);
 
 /* Device-side fixed-point encode of float32 (Coder.encode_f32_vec, paillier.rs:162-169;
  * Coder::encode_f64, fixedpoint_paillier/src/lib.rs:148-168, 187-189).
@@ -153,8 +178,8 @@ fphe_status fphe_encrypt(fphe_ctx* ctx, const uint32_t* P, uint32_t lp, const ui
  * as fphe_encrypt.  With r == NULL (device-drawn obfuscation) the library draws
  * z_p (standing for r^q mod p) and z_q (for r^p mod q) uniformly in Z_p^* x Z_q^* instead
  * of r and runs only z^s mod s^2 per half: the same distribution of r^n mod n^2 whenever
- * gcd(q, p-1) = gcd(p, q-1) = 1, checked at context creation (env
- * FPHE_KH_DIRECT_Z=0 draws r instead).  An injected r always gives the integers above. */
+ * gcd(q, p-1) = gcd(p, q-1) = 1, checked at context creation (DESIGN.md §3;
+ * FPHE_OPT_KH_DIRECT_Z = 0 draws r instead).  An injected r always gives the integers above. */
 fphe_status fphe_encrypt_crt(fphe_ctx* ctx, const uint32_t* P, uint32_t lp, const uint8_t* neg,
                              size_t count, const uint32_t* r, const uint32_t rng_key[8],
                              uint64_t rng_nonce, uint32_t* C, uint8_t* sign, void* stream);

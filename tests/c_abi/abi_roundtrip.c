@@ -5,6 +5,8 @@
  *
  * stdin : key_bits, n, p, q (hex), count, then `count` lines "<signed sig hex> <r hex>"
  * stdout: per element "<signed ciphertext hex> <decrypted significand hex>"
+ * argv[1]: "latency" or "throughput" selects the kernels of the encrypt and the decrypt
+ *          (fphe_ctx_set_option; default: the library's size thresholds)
  * tests/test_gpu_c_abi.py feeds it the golden fixture and compares with the oracle's values. */
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
@@ -52,7 +54,7 @@ static void* dalloc(size_t bytes) {
   return p;
 }
 
-int main(void) {
+int main(int argc, char** argv) {
   unsigned bits = 0;
   size_t count = 0;
   static char buf[8192], rbuf[8192];
@@ -68,6 +70,15 @@ int main(void) {
 
   fphe_ctx* ctx = NULL;
   CHECK(fphe_ctx_create(0, bits, n, p, q, &ctx));
+  if (argc > 1) {
+    const int64_t wide = strcmp(argv[1], "latency") == 0 ? (int64_t)1 << 20 : 0;
+    if (!wide && strcmp(argv[1], "throughput") != 0) return 1;
+    CHECK(fphe_ctx_set_option(ctx, FPHE_OPT_WIDE_ENCRYPT_MAX, wide));
+    CHECK(fphe_ctx_set_option(ctx, FPHE_OPT_WIDE_DECRYPT_MAX, wide));
+    int64_t got = -1;
+    CHECK(fphe_ctx_get_option(ctx, FPHE_OPT_WIDE_DECRYPT_MAX, &got));
+    if (got != wide) return 3;
+  }
   uint32_t L2 = 0, L1 = 0;
   CHECK(fphe_ctx_limbs(ctx, &L2, &L1));
   const size_t T = (count + 63) / 64;

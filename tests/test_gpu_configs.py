@@ -32,7 +32,7 @@ def _config1_inputs():
 
 
 @pytest.mark.parametrize("keyholder", [False, True], ids=["public", "keyholder_crt"])
-def test_config1_roundtrip_bit_exact(keyholder):
+def test_config1_roundtrip_bit_exact(keyholder, kernel_path):
     with open(os.path.join(HERE, "golden", "paillier_1024.json")) as f:
         fx = json.load(f)
     p, q = int(fx["p"], 16), int(fx["q"], 16)

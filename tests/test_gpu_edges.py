@@ -551,7 +551,7 @@ def test_mul_spans_match_one_launch(monkeypatch):
     assert torch.allclose(d, (x.double() * w.double()).cpu(), rtol=1e-6, atol=1e-6)
 
 
-def test_config2_subset_4096_vs_gmp():
+def test_config2_subset_4096_vs_gmp(kernel_path):
     """SURVEY.md §8(d) config 2's bit-exact subset at full size: the first 4,096 elements of the
     bench's 1M float32 tensor (randn * 4, seed 20241218, the edge values up front) at 2048
     bits, with injected obfuscation nonces: the public-key encrypt, the key-holder (CRT)

@@ -76,7 +76,7 @@ def test_iupdate(env):
     assert js(pk, v) == t["out"]
 
 
-def test_pack_squeeze(env):
+def test_pack_squeeze(env, kernel_path):
     ops, pk = env
     t = ops["pack_squeeze"]
     assert js(pk, vec(pk, t["data"]).pack_squeeze(t["pack_num"], t["shift_bit"], pk)) == t["out"]

@@ -53,7 +53,7 @@ def test_encode_f32(fx):
 
 
 @pytest.mark.parametrize("keyholder", [False, True], ids=["public", "keyholder_crt"])
-def test_encrypt_injected_r(fx, keyholder):
+def test_encrypt_injected_r(fx, kernel_path, keyholder):
     """Public-key path (fphe_encrypt) and key-holder CRT path (fphe_encrypt_crt): both must
     give the reference's ciphertext integers for the same r."""
     f, sk, pk, coder = fx
@@ -77,7 +77,7 @@ def test_encrypt_nude(fx):
     assert [hex(c) for c in cs] == e["nude"]
 
 
-def test_decrypt_and_decode(fx):
+def test_decrypt_and_decode(fx, kernel_path):
     f, sk, pk, coder = fx
     e = f["encrypt"]
     ct = P.CiphertextVector.from_signed_ints([int(c, 16) for c in e["ct"]], e["exp"], pk.ns, pk._key.L2)
@@ -104,7 +104,7 @@ def test_mul(fx):
 
 
 @pytest.mark.parametrize("keyholder", [False, True], ids=["public", "keyholder_crt"])
-def test_roundtrip_device_rng(fx, keyholder):
+def test_roundtrip_device_rng(fx, kernel_path, keyholder):
     """decrypt(encrypt(x)) == x with device-drawn r (reference test crates/paillier/src/lib.rs:190-197)."""
     f, sk, pk, coder = fx
     if not keyholder:
@@ -122,7 +122,7 @@ def test_roundtrip_device_rng(fx, keyholder):
     assert not torch.equal(ct.C, ct2.C)
 
 
-def test_keyholder_obfuscation_is_uniform_nth_residue(fx):
+def test_keyholder_obfuscation_is_uniform_nth_residue(fx, kernel_path):
     """The key holder's device-drawn obfuscation (k_draw_z: (z_p, z_q) drawn directly in CRT
     coordinates instead of r) is an n-th residue, x = c / (1 + m n) mod n^2 with x^lambda = 1
     mod n^2, as the reference's r^n (paillier/src/lib.rs:94-98), and since x mod p = z_p

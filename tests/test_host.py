@@ -134,6 +134,31 @@ def test_chacha20_reference_pinned_by_rfc8439():
     assert b"".join(w.to_bytes(4, "little") for w in got) == RFC8439_232_SERIALIZED
 
 
+def test_chacha20_vectorised_and_draws_match_scalar():
+    """The vectorised block function (tests/chacha_ref.chacha20_blocks_np) equals the scalar
+    one on RFC 8439's vector and other counters / nonces, and draw_below_host follows the
+    library's stream layout: element e, attempt 0 reads blocks (b | tag, (e, nonce hi, lo)),
+    keeps bits(bound) bits and accepts x < bound - 1 as r = x + 1 (random.rs:22-25)."""
+    import numpy as np
+    from tests.chacha_ref import (DRAW_Z_TAG, RFC8439_232, chacha20_block, chacha20_blocks_np,
+                                  draw_below_host)
+    key, counter, nonce, want = RFC8439_232
+    ctrs = [counter, 0, 7, 0xFFFFFFFF, 1 << 31]
+    nonces = [nonce, [1, 2, 3], [0, 0, 0], [0xFFFFFFFF] * 3, [5, 0xDEADBEEF, 9]]
+    got = chacha20_blocks_np(key, ctrs, nonces)
+    assert got[0].tolist() == want
+    for i in range(len(ctrs)):
+        assert got[i].tolist() == chacha20_block(key, ctrs[i], nonces[i])
+    bound = (1 << 200) - 12345  # acceptance ~1: attempt 0 for every element
+    nonce64 = (7 << 32) | 11
+    r = draw_below_host(key, nonce64, 5, bound, 8, DRAW_Z_TAG)
+    for e in range(5):
+        w = chacha20_block(key, DRAW_Z_TAG, [e, 7, 11])[:8]
+        x = int.from_bytes(np.array(w, dtype="<u4").tobytes(), "little") & ((1 << 200) - 1)
+        assert r[e] == (x + 1 if x < bound - 1 else r[e])
+        assert 1 <= r[e] < bound
+
+
 def test_chacha20_symbol_exported():
     from fate_amd import _lib
     assert "fphe_chacha20_blocks" in _lib.EXPORTED_SYMBOLS
