@@ -529,6 +529,85 @@ def hetero_lr_leg(P, pk, sk, coder, N, F, rank, dev):
             "gradient_allclose": bool(torch.allclose(got, want, rtol=1e-9, atol=1e-9))}
 
 
+def config5_leg(P, pk, sk, coder, dev, stream, meter, per_rank: int, rank: int, world: int, barrier) -> dict:
+    """BASELINE config 5 in weak form (12.5M elements per GPU, 100M at 8 GPUs):
+    each rank encrypts its contiguous shard [rank * per_rank, (rank + 1) * per_rank) of one
+    float32 vector (randn * 4, the bench's distribution, seeded by the shard's start), one
+    timed pass bracketed by a barrier and a device synchronise, max over ranks; then the
+    exchange step of python/fate/arch/tensor/distributed/_tensor.py:365-395 over RCCL: the
+    whole vector onto rank 0 (the federation sender; fate_amd.dist.gather_tiles_to, point to
+    point) and onto every rank (the all-gather, fate_amd.dist.gather_tiles).  A 4,096-element
+    sample decrypts to its inputs' bits."""
+    s0 = rank * per_rank
+    g = torch.Generator().manual_seed(20241218 + s0)
+    x = torch.randn(per_rank, generator=g, dtype=torch.float32) * 4
+    if rank == 0:
+        x[:8] = torch.tensor([0.0, -0.0, 1e-30, -1e-30, 3.4e38, -3.4e38, 1.0, -1.0])[:per_rank]
+    xd = x.to(dev)
+    barrier()
+    st0 = meter.stamp()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    ct = pk.encrypt_encoded(coder.encode_f32_vec(xd), True)
+    e1.record(stream)
+    st1 = meter.stamp()
+    barrier()
+    secs = time.perf_counter() - t0
+    kms = e0.elapsed_time(e1)
+    clock = meter.ghz(st0, st1)
+    nchk = min(per_rank, 4096)
+    y = coder.decode_f32_vec(sk.decrypt_to_encoded(ct._gather(torch.arange(nchk)))).cpu().numpy().view(np.uint32)
+    xb = x[:nchk].numpy().view(np.uint32).copy()
+    xb[xb == 0x80000000] = 0
+    ok = bool(np.array_equal(y, xb))
+    del xd, x
+    out = {"elements_per_rank": per_rank, "elements_total": per_rank * world, "ranks": world,
+           "scaling": "weak", "seconds": None, "encrypts_per_s": None,
+           "per_rank": {"encrypt_kernel_ms": [round(kms, 3)], "clock_GHz": [clock["GHz"] if clock else None]},
+           "sample_roundtrip_bit_exact": ok}
+    if world > 1:
+        import torch.distributed as tdist
+        tt = torch.tensor([secs, kms, clock["GHz"] if clock else float("nan"), 1.0 if ok else 0.0],
+                          dtype=torch.float64, device=dev)
+        allr = [torch.empty_like(tt) for _ in range(world)]
+        tdist.all_gather(allr, tt)
+        secs = max(float(v[0]) for v in allr)
+        ks = [float(v[1]) for v in allr]
+        out["per_rank"] = {"encrypt_kernel_ms": [round(v, 3) for v in ks],
+                           "clock_GHz": [round(float(v[2]), 4) for v in allr],
+                           "kernel_ms_spread": round(max(ks) / min(ks), 4)}
+        out["sample_roundtrip_bit_exact"] = all(float(v[3]) == 1.0 for v in allr)
+        from fate_amd.dist import gather_tiles, gather_tiles_to
+        per_elem = ct.C.shape[1] * 4 + 1 + 4
+        for name, fn in (("gather_to_rank0", lambda: gather_tiles_to(ct.C, ct.sign, ct.exp, ct.count, 0, trim=False)),
+                         ("allgather", lambda: gather_tiles(ct.C, ct.sign, ct.exp, ct.count, trim=False))):
+            torch.cuda.empty_cache()
+            barrier()
+            tg = time.perf_counter()
+            got = fn()
+            barrier()
+            gs = time.perf_counter() - tg
+            tt = torch.tensor([gs], dtype=torch.float64, device=dev)
+            tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
+            gs = float(tt.item())
+            total = sum(got[3]) if got is not None else per_rank * world
+            recv = (total - ct.count) * per_elem
+            out[name] = {"seconds": round(gs, 4), "elements": int(total), "bytes_per_elem": per_elem,
+                         "recv_GB": round(recv / 1e9, 2), "recv_GBps": round(recv / gs / 1e9, 2),
+                         "encrypt_plus_exchange_per_s": round(per_rank * world / (secs + gs), 1)}
+            del got
+    out["seconds"] = round(secs, 4)
+    out["encrypts_per_s"] = round(per_rank * world / secs, 1)
+    out["kernel_ms_rank0"] = round(kms, 3)
+    out["frac"] = round(per_rank * enc_mac32_per_elem(pk.n.bit_length()) / (kms / 1e3) / 1e12 / PEAK_TMAC32, 4)
+    out.update(at_clock(out["frac"], clock))
+    del ct
+    torch.cuda.empty_cache()
+    return out
+
+
 def launch_ranks(nproc: int) -> int:
     """`bench.py --gpus N` (N > 1) started without a launcher: run the same command line as N
     ranks under torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1) and
@@ -566,6 +645,9 @@ def main() -> None:
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the ciphertext all-gather leg")
     ap.add_argument("--config4-samples", type=int, default=10_000_000,
                     help="BASELINE config 4 leg (histogram_config4): samples in all, split over the ranks; 0 skips it")
+    ap.add_argument("--config5-per-rank", type=int, default=12_500_000,
+                    help="BASELINE config 5 leg (config5): elements per rank (weak: 100M at 8 GPUs), "
+                         "then gather to rank 0 and all-gather; 0 skips it")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -1049,6 +1131,13 @@ def main() -> None:
             extras["histogram_config4"] = sbf.config4(P, pk_kh, sk, coder, dev, total=args.config4_samples, rank=rank,
                                                       world=world, iupdate_roofline=iupdate_roofline)
             torch.cuda.empty_cache()
+
+    # BASELINE config 5 (every line, so the driver's scaling run measures it): 12.5M per rank
+    if args.config5_per_rank > 0 and not strong:
+        del ct
+        torch.cuda.empty_cache()
+        extras["config5"] = config5_leg(P, pk, sk, coder, dev, stream, meter, args.config5_per_rank, rank, world,
+                                        barrier)
 
     if rank != 0:
         if dist:

@@ -1,9 +1,10 @@
-"""Multi-process (world_size 2, gloo, CPU) tests of the element sharding and the ciphertext
+"""Multi-process (world sizes 2, 4 and 8, gloo, CPU) tests of the element sharding and the ciphertext
 all-gather used for N>1 GPUs (fate_amd/dist.py).  The data-path collective is exercised on
 CPU tensors in the same tile-major layout the GPU kernels produce."""
 import os
 import socket
 
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -69,18 +70,31 @@ def _worker(rank, world, port, count, L, q):
         dist.destroy_process_group()
 
 
-def test_gather_tiles_world2():
+def _run(target, world, *args, timeout=300):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    count, L, world = 200, 5, 2  # rank 0: 128 (2 tiles), rank 1: 72 (partial last tile)
-    procs = [ctx.Process(target=_worker, args=(r, world, port, count, L, q)) for r in range(world)]
+    procs = [ctx.Process(target=target, args=(r, world, port, *args, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=120) for _ in range(world))
-    for p in procs:
-        p.join(timeout=60)
-    assert res == {0: True, 1: True}
+    try:
+        res = dict(q.get(timeout=timeout) for _ in range(world))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    return res
+
+
+@pytest.mark.parametrize("world,count", [(2, 200), (4, 333), (8, 200), (8, 1000)])
+def test_gather_tiles(world, count):
+    """The all-gather and the gather onto each rank in turn.  Ragged shards: 200 elements at
+    world 2 are 128 + 72 (a partial last tile); at world 8 they are 4 tiles over 8 ranks, so
+    four ranks hold nothing; 333 at world 4 and 1000 at world 8 end in partial tiles."""
+    L = 5
+    res = _run(_worker, world, count, L)
+    assert res == {r: True for r in range(world)}
 
 
 def test_compact_gathered_ragged_and_whole_tiles():
@@ -174,17 +188,11 @@ def _fold_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_cross_rank_ciphertext_fold_world2():
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_cross_rank_ciphertext_fold(world):
     """SecureBoost's histogram across GPUs: per-rank partial folds,
     all-gathered, then folded again with ct-add; bit-exact against a fold of the same
-    partials in another order, on world_size 2 over gloo."""
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_fold_worker, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    res = dict(q.get(timeout=300) for _ in range(2))
-    for p in procs:
-        p.join(timeout=60)
-    assert res == {0: True, 1: True}
+    partials in another order -- what one rank folding every sample
+    gives -- over gloo at world sizes 2, 4 and 8 (config 4's 8-way split)."""
+    res = _run(_fold_worker, world)
+    assert res == {r: True for r in range(world)}

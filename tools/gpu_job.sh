@@ -15,6 +15,7 @@
 #       evidence  round, then prof, then pmc (the end-of-round record for profiles/)
 #       final     prof, pmc, then the 2-rank gloo rehearsal of the N > 1 bench line on the one GPU
 #                 (after `round`: the rest of the end-of-round record)
+#       gloo2     the 2-rank gloo rehearsal alone (config 5 at 1M per rank)
 #       leg       python tools/bench_legs/ARGS (one bench leg script)
 #       timeline  rocprofv3 kernel trace of tools/bench_legs/hist_leg.py ARGS (PHASES=0), last
 #                 TL_LAST (90) dispatches as a timeline
@@ -75,6 +76,12 @@ run_sq() {
   echo sq_ok
 }
 
+run_gloo2() {  # the N > 1 bench line rehearsed with two gloo ranks sharing the one GPU
+  FPHE_DIST_BACKEND=gloo timeout -k 10 600 python -u bench.py --gpus 2 --steps 1 --warmup 1 --config4-samples 400000 --config5-per-rank 1000000 > gpurun_out/${T}_gloo2.txt 2>&1 || { echo gloo_failed; tail -20 gpurun_out/${T}_gloo2.txt; exit 1; }
+  grep '^{"metric"' gpurun_out/${T}_gloo2.txt | tail -1 > gpurun_out/${T}_gloo2.json
+  python -c "import json; d=json.load(open('gpurun_out/${T}_gloo2.json')); print(d['n_gpus'], d['value'], d.get('per_rank'), d.get('allgather'), d.get('histogram_multi_gpu'), d.get('config5'))"
+}
+
 case $M in
   tests) run_tests "$@" ;;
   round) run_tests; run_smoke; run_bench "$@" ;;
@@ -98,11 +105,8 @@ for k, v in sorted(agg.items(), key=lambda kv: kv[0][1]):
 PYEOF
     ;;
   evidence) run_tests; run_smoke; run_bench "$@"; run_prof; run_pmc ;;
-  final)
-    run_prof; run_pmc
-    FPHE_DIST_BACKEND=gloo timeout -k 10 600 python -u bench.py --gpus 2 --steps 1 --warmup 1 --config4-samples 400000 > gpurun_out/${T}_gloo2.txt 2>&1 || { echo gloo_failed; tail -20 gpurun_out/${T}_gloo2.txt; exit 1; }
-    grep '^{"metric"' gpurun_out/${T}_gloo2.txt | tail -1 > gpurun_out/${T}_gloo2.json
-    python -c "import json; d=json.load(open('gpurun_out/${T}_gloo2.json')); print(d['n_gpus'], d['value'], d.get('per_rank'), d.get('allgather'), d.get('histogram_multi_gpu'))" ;;
+  final) run_prof; run_pmc; run_gloo2 ;;
+  gloo2) run_gloo2 ;;
   timeline)  # kernel timeline of the last ~90 dispatches of a histogram leg: args go to hist_leg.py
     (cd /tmp && export TMPDIR=/tmp PHASES=0 && timeout -k 10 600 rocprofv3 --kernel-trace --output-format rocpd -d $R/gpurun_out/${T}_kt -o run -- python3 $R/tools/bench_legs/hist_leg.py "$@" > $R/gpurun_out/${T}_kt.txt 2>&1) || { echo timeline_failed; tail -20 gpurun_out/${T}_kt.txt; exit 1; }
     python tools/rocpd_timeline.py $(ls gpurun_out/${T}_kt/*.db gpurun_out/${T}_kt/*/*.db 2>/dev/null | head -1) ${TL_LAST:-90} > gpurun_out/${T}_timeline.txt
