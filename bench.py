@@ -42,6 +42,16 @@ CPU_SHARE_PER_GPU = 16
 ENGINE_LL = 37
 
 
+_T_START = time.perf_counter()
+
+
+def progress(msg: str) -> None:
+    """One line per leg on stderr (the JSON line stays alone on stdout): a run that prints
+    nothing for minutes is taken to be hung by the GPU harness."""
+    r = os.environ.get("RANK", "0")
+    print(f"[bench r{r} {time.perf_counter() - _T_START:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def mac32_per_mont(L: int) -> int:
     return 2 * L * L + L
 
@@ -706,12 +716,14 @@ def main() -> None:
         pv = coder.encode_f32_vec(xd)
         return pk.encrypt_encoded(pv, True)
 
+    progress(f"inputs ready: {N} elements per rank")
     # warmup (also allocates the modexp scratch)
     ct = None
     for _ in range(max(args.warmup, 0)):
         ct = step()
     barrier()
 
+    progress("warm-up done")
     # timed region; HIP events on the stream the kernels are launched on, and shader-clock
     # stamps (fphe_clock_stamp: two one-wave launches, microseconds) around the steps
     meter = ClockMeter(dev, stream)
@@ -749,6 +761,7 @@ def main() -> None:
                     "kernel_ms_min": round(min(ks), 3), "kernel_ms_max": round(max(ks), 3),
                     "kernel_ms_spread": round(max(ks) / min(ks), 4),
                     "clock_GHz_min": round(min(cs), 4), "clock_GHz_max": round(max(cs), 4)}
+    progress(f"timed encrypt: {args.steps} steps in {elapsed:.1f} s")
     value = (args.total if strong else world * N) * args.steps / elapsed
 
     # BASELINE config 5's exchange step, outside the timed region: every rank's ciphertext
@@ -815,6 +828,7 @@ def main() -> None:
         xb = x.numpy().view(np.uint32).copy()
         xb[xb == 0x80000000] = 0  # -0.0 encodes to significand 0 -> decodes +0.0 (reference)
         roundtrip_ok = bool(np.array_equal(y.cpu().numpy().view(np.uint32), xb))
+        progress("decrypt leg done")
         # ct-add (Hetero-LR aggregate shape): enc(x) + enc(0.25*x') elementwise, exps differ
         ct2 = pk.encrypt_encoded(coder.encode_f32_vec(torch.flip(xd, [0]) * 0.25), True)
         for _ in range(4):  # untimed: first-call costs of the sort, the output's allocation, the clock
@@ -874,6 +888,7 @@ def main() -> None:
                           "scope": "host f32 (pinned) -> H2D -> device encode + obfuscated encrypt -> export of the "
                                    "signed integers -> device bincode formatting -> D2H into pinned host bytes"}
         del cw, wrec, Wh, back
+        progress("ct-add, end-to-end and wire legs done")
         # ct x pt (SecureBoost GOSS-style weights; negatives take the device inverse branch)
         gw = torch.Generator().manual_seed(777 + rank)
         wts = (torch.rand(N, generator=gw, dtype=torch.float32) * 3.0 - 1.0).to(dev)
@@ -928,6 +943,7 @@ def main() -> None:
             fin = torch.isfinite(want)
             return hh, secs, bool(torch.allclose(hd[fin], want[fin], rtol=1e-9, atol=1e-6)), want
 
+        progress("ct x pt leg done")
         hist_clock = []
         hist, hist_s, hist_ok, want = run_hist(gh, g_sb.double(), h_sb.double())
         hist_h = P.CiphertextVector.zeros(HF * NB * 2, pk._key.L2, dev)
@@ -998,8 +1014,10 @@ def main() -> None:
                 del acc
             except Exception as exc:  # report, do not take the scaling run down
                 hist_mgpu = {"error": repr(exc)[:200]}
+        progress("histogram legs done")
         packed = hist_packed_leg(P, pk_kh, sk, coder, N, HF, NB, key_bits, rank, dev)
         hlr = hetero_lr_leg(P, pk, sk, coder, N, 4, rank, dev)
+        progress("packed histogram and Hetero-LR legs done")
         # 1024-bit keys (the reference's own tests and configs[0] use them)
         with open(os.path.join(ROOT, "tests", "golden", "paillier_1024.json")) as f:
             fx1 = json.load(f)
@@ -1052,6 +1070,7 @@ def main() -> None:
                      "encrypt_roofline_frac": round(n4 * enc_mac32_per_elem(4096) / (enc4_ms / 1e3) / 1e12 / PEAK_TMAC32, 4),
                      "decrypt_roofline_frac": round(n4 * dec_mac32_per_elem(4096) / (dec4_ms / 1e3) / 1e12 / PEAK_TMAC32, 4)}
             del c4, d4, y4, pv4
+        progress("1024- and 4096-bit legs done")
         # key-holder encryption (CRT halves): throughput, round trip, and identity with the
         # public-key path on a subset with the same injected r
         torch.cuda.synchronize(dev)
@@ -1121,6 +1140,7 @@ def main() -> None:
         # BASELINE config 4 at its stated size (10M samples x 10 features x 32 bins, 2048-bit):
         # unpacked ct x pt + the 200M-term iupdate, packed iupdate + cumsum + squeeze, sharded
         # over the ranks with the cross-rank fold (tools/bench_legs/secureboost_full.py)
+        progress("key-holder leg done")
         if args.config4_samples > 0:
             import importlib.util
             spec = importlib.util.spec_from_file_location(
@@ -1132,6 +1152,7 @@ def main() -> None:
                                                       world=world, iupdate_roofline=iupdate_roofline)
             torch.cuda.empty_cache()
 
+    progress("extras done")
     # BASELINE config 5 (every line, so the driver's scaling run measures it): 12.5M per rank
     if args.config5_per_rank > 0 and not strong:
         del ct
@@ -1197,6 +1218,7 @@ def main() -> None:
         out["per_rank"] = per_rank
     out.update(gather_info)
     out.update(extras)
+    progress("config 5 leg done; CPU baseline next" if world == 1 else "config 5 leg done")
     if world == 1 and not args.no_cpu_baseline and not strong:
         try:
             cb = cpu_baseline(p, q)

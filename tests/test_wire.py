@@ -240,6 +240,58 @@ print(json.dumps(out))
                                                              "fate_utils.paillier.Coder"]
 
 
+def test_alias_pickles_load_with_and_without_install(tmp_path):
+    """install() leaves fate_amd.paillier's classes alone (alias subclasses
+    plus copyreg reducers instead of rewriting __module__).  Objects pickled in an installed
+    process load in an installed process and in one that never called install() (fate_amd's
+    fallback finder serves the aliases when no real fate_utils exists), while a real fate_utils
+    on sys.path still wins over the aliases."""
+    import subprocess
+    import sys
+    root, fx = os.path.dirname(HERE), os.path.join(HERE, "golden", "paillier_1024.json")
+    blob = tmp_path / "objs.pkl"
+    head = f"import sys, json, pickle\nsys.path.insert(0, {root!r})\n"
+    dump = head + f"""
+import fate_amd.paillier as P
+from fate_amd import compat
+fx = json.load(open({fx!r}))
+sk, pk, coder = P.keypair_from_primes(int(fx["p"], 16), int(fx["q"], 16))
+compat.install()
+assert P.PK.__module__ == "fate_amd.paillier" and P.CiphertextVector.__module__ == "fate_amd.paillier"
+b = pickle.dumps((pk, sk, coder, P.Evaluator()))
+assert b"fate_amd" not in b and b"fate_utils.paillier" in b
+open({str(blob)!r}, "wb").write(b)
+print(json.dumps([pk.__getstate__().hex(), sk.__getstate__().hex(), coder.__getstate__().hex()]))
+"""
+    load = head + f"""
+INSTALL = int(sys.argv[1])
+import fate_amd.paillier as P
+if INSTALL:
+    from fate_amd import compat
+    compat.install()
+objs = pickle.load(open({str(blob)!r}, "rb"))
+assert [type(o).__module__ + "." + type(o).__name__ for o in objs] == [
+    "fate_utils.paillier.PK", "fate_utils.paillier.SK", "fate_utils.paillier.Coder", "fate_utils.paillier.Evaluator"]
+assert isinstance(objs[0], P.PK) and isinstance(objs[1], P.SK) and isinstance(objs[2], P.Coder)
+print(json.dumps([o.__getstate__().hex() for o in objs[:3]]))
+"""
+    r = subprocess.run([sys.executable, "-c", dump], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    want = json.loads(r.stdout.strip().splitlines()[-1])
+    for install in ("1", "0"):
+        r = subprocess.run([sys.executable, "-c", load, install], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, (install, r.stderr[-2000:])
+        assert json.loads(r.stdout.strip().splitlines()[-1]) == want
+    # a real fate_utils (here a stand-in package on sys.path) is found before the aliases
+    real = tmp_path / "site" / "fate_utils"
+    real.mkdir(parents=True)
+    (real / "__init__.py").write_text("REAL = True\n")
+    probe = head + f"sys.path.insert(0, {str(tmp_path / 'site')!r})\nimport fate_amd\nimport fate_utils\n" \
+        "assert getattr(fate_utils, 'REAL', False) and not getattr(fate_utils, '_fate_amd_alias', False)\n"
+    r = subprocess.run([sys.executable, "-c", probe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("bits", [1024, 2048])
 def test_ciphertext_and_plaintext_vector_pickle(bits):
