@@ -1201,6 +1201,7 @@ fphe_status launch_fold_segments(fphe_ctx* c, const u32* Src, const u8* ssign, c
   if (hipMemcpyAsync(h, mm, sizeof(h), hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
     return FPHE_ERR_HIP;
   if (h[2]) return FPHE_ERR_ARG;  // an index or segment out of range
+  const int32_t emin = h[0];  // (h is reused for later read-backs)
   const int64_t NE = (int64_t)h[1] - h[0] + 1;
   if (NE < 1 || (size_t)NE * nseg > kMaxFoldKeys) return FPHE_ERR_RANGE;
   const size_t nkeys = (size_t)NE * nseg;
@@ -1234,11 +1235,11 @@ fphe_status launch_fold_segments(fphe_ctx* c, const u32* Src, const u8* ssign, c
                        R, keys, cntR);
   if (dev_scan(c, cntR, nkeys * R, offR, nullptr, B) != FPHE_OK) return FPHE_ERR_HIP;
   if (lds_counts)
-    hipLaunchKernelGGL(k_gr_bscatter, dim3(nbc), dim3(kGrBlock), nkeys * 4, s, keys, idx, T, (int32_t)nkeys, offR, fill,
-                       ord, skey);
+    hipLaunchKernelGGL(k_gr_bscatter, dim3(nbc), dim3(kGrBlock), nkeys * 4, s, keys, idx, ssign, T, (int32_t)nkeys,
+                       offR, fill, ord, skey);
   else
-    hipLaunchKernelGGL(k_gr_scatter, dim3(gr_grid(T, c->cus)), dim3(kGrBlock), 0, s, keys, idx, T, R, offR, fill, ord,
-                       skey);
+    hipLaunchKernelGGL(k_gr_scatter, dim3(gr_grid(T, c->cus)), dim3(kGrBlock), 0, s, keys, idx, ssign, T, R, offR, fill,
+                       ord, skey);
   // 4. fold every (segment, exponent) run to one partial.  First level: the sorted items in
   // equal ranges of r per wave slot, whatever the runs (k_segfold27: balanced, a whole number
   // of wave rounds); then chunk levels per key until one partial is left per key.
@@ -1325,7 +1326,7 @@ fphe_status launch_fold_segments(fphe_ctx* c, const u32* Src, const u8* ssign, c
   P.key = B.get<int32_t>(ub1);
   if (!B.ok || sj.join() != FPHE_OK) return FPHE_ERR_HIP;
   hipLaunchKernelGGL(ksf, dim3(occ_grid(c, ksf, lds, (nslots + E - 1) / E, "segfold")), dim3(kBlock), lds, s, c->K,
-                     rows, ssign, sexp, ord, skey, T, (u32)r, (const int32_t*)plan, poff, P.rows, P.sign, P.exp, P.key,
+                     rows, emin, (int32_t)NE, ord, skey, T, (u32)r, (const int32_t*)plan, poff, P.rows, P.sign, P.exp, P.key,
                      (u32)NL);
   P.cnt = cnt2;
   P.off = off2;

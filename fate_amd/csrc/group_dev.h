@@ -232,23 +232,28 @@ __global__ __launch_bounds__(kGrBlock) void k_scan_add(int32_t* __restrict__ out
 // --- pass 3: counting-sort scatter ------------------------------------------------------------
 // ord[off[key * R + c] + rank] = source index of the term (rank by an atomic cursor of the
 // term's copy c: the order within a key is arbitrary, the fold does not depend on it)
+// skey (may be null) gets the sorted keys with the term's sign in bit 31 (ssign non-null; keys
+// stay below 2^25): the fold's first level then reads neither the source's sign nor its
+// exponent per term (the exponent is the key's), only its row.
 __global__ __launch_bounds__(kGrBlock) void k_gr_scatter(const int32_t* __restrict__ keys, const int32_t* __restrict__ idx,
-                                                         size_t T, int32_t R, const int32_t* __restrict__ off,
-                                                         int32_t* __restrict__ fill, int32_t* __restrict__ ord,
-                                                         int32_t* __restrict__ skey) {
+                                                         const u8* __restrict__ ssign, size_t T, int32_t R,
+                                                         const int32_t* __restrict__ off, int32_t* __restrict__ fill,
+                                                         int32_t* __restrict__ ord, int32_t* __restrict__ skey) {
   for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < T; t += (size_t)gridDim.x * blockDim.x) {
     const int32_t k = keys[t];
     const size_t kc = (size_t)k * R + ((t >> kCopyShift) % R);
     const int32_t pos = off[kc] + atomicAdd(&fill[kc], 1);
-    ord[pos] = idx ? idx[t] : (int32_t)t;
-    if (skey) skey[pos] = k;
+    const int32_t src = idx ? idx[t] : (int32_t)t;
+    ord[pos] = src;
+    if (skey) skey[pos] = k | (ssign && ssign[src] ? (int32_t)0x80000000u : 0);
   }
 }
 
 // k_gr_bkeys' scatter: each term's rank within its block and key from an LDS atomic, one global
 // cursor reservation per non-zero (block, key), then ord[off[key] + base + rank]
 __global__ __launch_bounds__(kGrBlock) void k_gr_bscatter(const int32_t* __restrict__ keys, const int32_t* __restrict__ idx,
-                                                          size_t T, int32_t nkeys, const int32_t* __restrict__ off,
+                                                          const u8* __restrict__ ssign, size_t T, int32_t nkeys,
+                                                          const int32_t* __restrict__ off,
                                                           int32_t* __restrict__ fill, int32_t* __restrict__ ord,
                                                           int32_t* __restrict__ skey) {
   extern __shared__ int32_t hist[];
@@ -274,8 +279,9 @@ __global__ __launch_bounds__(kGrBlock) void k_gr_bscatter(const int32_t* __restr
     if (kk[i] < 0) continue;
     const size_t t = t0 + (size_t)i * kGrBlock;
     const int32_t pos = hist[kk[i]] + rk[i];
-    ord[pos] = idx ? idx[t] : (int32_t)t;
-    if (skey) skey[pos] = kk[i];
+    const int32_t src = idx ? idx[t] : (int32_t)t;
+    ord[pos] = src;
+    if (skey) skey[pos] = kk[i] | (ssign && ssign[src] ? (int32_t)0x80000000u : 0);  // as k_gr_scatter
   }
 }
 
@@ -339,9 +345,9 @@ __global__ __launch_bounds__(kGrBlock) void k_gr_segcount(const int32_t* __restr
       pcnt[i] = 0;
       continue;
     }
-    int32_t k = skey[p0], np = 1;
+    int32_t k = skey[p0] & 0x7fffffff, np = 1;  // bit 31: the term's sign (k_gr_bscatter)
     for (size_t p = p0 + 1; p < p1; ++p) {
-      const int32_t kp = skey[p];
+      const int32_t kp = skey[p] & 0x7fffffff;
       if (kp != k) {
         atomicAdd(&cnt2[k], 1);
         k = kp;

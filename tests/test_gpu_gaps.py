@@ -163,3 +163,21 @@ def test_forced_raise_skips_gap_beyond_kernel_limit(k1024, monkeypatch):
     want = [O.ct_zero() for _ in range(2)]
     O.iupdate(opk, want, [O.Ciphertext(c, e) for c, e in zip(cs, exps)], positions, 1)
     assert hist.to_signed_ints(pk.ns) == ([w.c for w in want], [w.exp for w in want])
+
+
+def test_stale_exponent_bound_is_caught(k1024):
+    """ct-add skips the gap read-back when the host-side bounds (ebound) keep every
+    gap within the kernel's exact range.  With FPHE_CHECK_EBOUND=1 (set for the test suite,
+    tests/conftest.py) a bound that no longer covers the exponents fails loudly instead of
+    giving a silently wrong sum."""
+    sk, pk, coder, osk, opk, _ = k1024
+    assert P.CHECK_EBOUND
+    x = torch.tensor([1.5, -2.25, 1e-20, 3e10], dtype=torch.float64).cuda()
+    a = pk.encrypt_encoded(coder.encode_f64_vec(x), True)
+    b = pk.encrypt_encoded(coder.encode_f64_vec(x * 0.5), True)
+    a.add(pk, b)  # sound bounds: passes
+    lo, hi = a.ebound
+    a.ebound = (hi, hi)  # stale: the exponents span [lo, hi] with lo < hi
+    assert lo < hi
+    with pytest.raises(AssertionError, match="stale exponent bound"):
+        a.add(pk, b)

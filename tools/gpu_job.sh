@@ -16,6 +16,7 @@
 #       final     prof, pmc, then the 2-rank gloo rehearsal of the N > 1 bench line on the one GPU
 #                 (after `round`: the rest of the end-of-round record)
 #       gloo2     the 2-rank gloo rehearsal alone (config 5 at 1M per rank)
+#       sqenc     SQ counter passes over the headline encrypt kernel alone
 #       leg       python tools/bench_legs/ARGS (one bench leg script)
 #       timeline  rocprofv3 kernel trace of tools/bench_legs/hist_leg.py ARGS (PHASES=0), last
 #                 TL_LAST (90) dispatches as a timeline
@@ -107,6 +108,14 @@ PYEOF
   evidence) run_tests; run_smoke; run_bench "$@"; run_prof; run_pmc ;;
   final) run_prof; run_pmc; run_gloo2 ;;
   gloo2) run_gloo2 ;;
+  sqenc)  # SQ counters of the headline encrypt (k_encrypt27<128,6>): wait shares, VMEM/LDS mix
+    ENC="python3 $R/bench.py --n 131072 --steps 1 --warmup 0 --no-extras --no-cpu-baseline --config5-per-rank 0"
+    pmc_pass sqe1 "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE GRBM_COUNT" $ENC
+    pmc_pass sqe2 "SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_LDS_BANK_CONFLICT SQ_INSTS_BRANCH SQ_WAVES" $ENC
+    python tools/pmc_sq_compare.py gpurun_out/${T}_sqe1 gpurun_out/${T}_sqe2 --match k_encrypt27 > gpurun_out/${T}_sqenc.txt || exit 1
+    pmc_pass sqe3 "SQ_INST_LEVEL_VMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES" $ENC
+    python tools/pmc_sq_compare.py gpurun_out/${T}_sqe3 --match k_encrypt27 >> gpurun_out/${T}_sqenc.txt || exit 1
+    cat gpurun_out/${T}_sqenc.txt ;;
   timeline)  # kernel timeline of the last ~90 dispatches of a histogram leg: args go to hist_leg.py
     (cd /tmp && export TMPDIR=/tmp PHASES=0 && timeout -k 10 600 rocprofv3 --kernel-trace --output-format rocpd -d $R/gpurun_out/${T}_kt -o run -- python3 $R/tools/bench_legs/hist_leg.py "$@" > $R/gpurun_out/${T}_kt.txt 2>&1) || { echo timeline_failed; tail -20 gpurun_out/${T}_kt.txt; exit 1; }
     python tools/rocpd_timeline.py $(ls gpurun_out/${T}_kt/*.db gpurun_out/${T}_kt/*/*.db 2>/dev/null | head -1) ${TL_LAST:-90} > gpurun_out/${T}_timeline.txt
