@@ -59,8 +59,8 @@ pmc_pass() {  # pmc_pass NAME COUNTER CMD...
   (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 300 rocprofv3 --pmc $counter --output-format csv -d $R/gpurun_out/${T}_${name} -o run -- "$@" > $R/gpurun_out/${T}_${name}.txt 2>&1) || { echo pmc_${name}_failed; tail -20 gpurun_out/${T}_${name}.txt; exit 1; }
 }
 run_pmc() {
-  pmc_pass pmc_fetch FETCH_SIZE python3 $R/bench.py --n 131072 --steps 1 --warmup 0 --no-extras --no-cpu-baseline
-  pmc_pass pmc_write WRITE_SIZE python3 $R/bench.py --n 131072 --steps 1 --warmup 0 --no-extras --no-cpu-baseline
+  pmc_pass pmc_fetch FETCH_SIZE python3 $R/bench.py --n 131072 --steps 1 --warmup 0 --no-extras --no-cpu-baseline --config5-per-rank 0
+  pmc_pass pmc_write WRITE_SIZE python3 $R/bench.py --n 131072 --steps 1 --warmup 0 --no-extras --no-cpu-baseline --config5-per-rank 0
   python tools/pmc_summary.py gpurun_out/$T gpurun_out/${T}_pmc_encrypt27.json > /dev/null || exit 1
   pmc_pass fetch FETCH_SIZE python3 $R/tools/bench_legs/ops_pmc_leg.py
   pmc_pass write WRITE_SIZE python3 $R/tools/bench_legs/ops_pmc_leg.py
