@@ -1177,22 +1177,31 @@ fphe_status launch_fold_segments(fphe_ctx* c, const u32* Src, const u8* ssign, c
   hipLaunchKernelGGL(k_gr_init_out<L>, dim3(g0), dim3(kGrBlock), 0, s, nseg, c->K.N2M1, Co, so, eo, present);
   if (T == 0) return hip_ok(hipGetLastError());
   // 1. element-major copy of the source (the fold gathers whole rows), on the context's side
-  // stream: it overlaps the exponent-range read-back and the counting sort below, and the
-  // stream joins it before the fold (or on any early return, before the scratch is freed)
+  // stream: it overlaps the counting sort below, and the stream joins it before the fold (or on
+  // any early return, before the scratch is freed).  It is forked before the exponent-range
+  // read-back, beside k_gr_minmax (which then shares HBM with it: ~0.3 ms).  Forking it after
+  // the read-back instead (FPHE_FOLD_COPY_EARLY=0) measured the same call time, 16.59 against
+  // 16.53 ms median over 12 alternating cold calls (profiles/r06/r06f_iupdate_ab_copy_late.txt)
   int32_t* mm = B.get<int32_t>(4);
   u32* rows = B.get<u32>(nsrc * L);
   if (!B.ok) return FPHE_ERR_HIP;
   SideJoin sj{c, s};
-  if (ensure_side(c) != FPHE_OK || hipEventRecord(c->ev_fork, s) != hipSuccess ||
-      hipStreamWaitEvent(c->side, c->ev_fork, 0) != hipSuccess)
-    return FPHE_ERR_HIP;
-  hipLaunchKernelGGL(k_tiles_to_rows<L>, dim3((unsigned)std::min<size_t>(ntiles_of(nsrc), (size_t)c->cus * 8)),
-                     dim3(kGrBlock), 0, c->side, Src, nsrc, rows);
-  if (hipEventRecord(c->ev_join, c->side) != hipSuccess) {
-    (void)hipStreamSynchronize(c->side);
-    return FPHE_ERR_HIP;
-  }
-  sj.armed = true;
+  auto fork_copy = [&]() -> fphe_status {
+    if (ensure_side(c) != FPHE_OK || hipEventRecord(c->ev_fork, s) != hipSuccess ||
+        hipStreamWaitEvent(c->side, c->ev_fork, 0) != hipSuccess)
+      return FPHE_ERR_HIP;
+    hipLaunchKernelGGL(k_tiles_to_rows<L>, dim3((unsigned)std::min<size_t>(ntiles_of(nsrc), (size_t)c->cus * 8)),
+                       dim3(kGrBlock), 0, c->side, Src, nsrc, rows);
+    if (hipEventRecord(c->ev_join, c->side) != hipSuccess) {
+      (void)hipStreamSynchronize(c->side);
+      return FPHE_ERR_HIP;
+    }
+    sj.armed = true;
+    return FPHE_OK;
+  };
+  const char* ce = getenv("FPHE_FOLD_COPY_EARLY");
+  const bool copy_early = !(ce && ce[0] == '0');
+  if (copy_early && fork_copy() != FPHE_OK) return FPHE_ERR_HIP;
   // 2. exponent range (one small read back: it sizes the key space)
   const int32_t mm0[4] = {kI32Max, kI32Min, 0, 0};
   if (hipMemcpyAsync(mm, mm0, sizeof(mm0), hipMemcpyHostToDevice, s) != hipSuccess) return FPHE_ERR_HIP;
@@ -1201,6 +1210,7 @@ fphe_status launch_fold_segments(fphe_ctx* c, const u32* Src, const u8* ssign, c
   if (hipMemcpyAsync(h, mm, sizeof(h), hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
     return FPHE_ERR_HIP;
   if (h[2]) return FPHE_ERR_ARG;  // an index or segment out of range
+  if (!copy_early && fork_copy() != FPHE_OK) return FPHE_ERR_HIP;
   const int32_t emin = h[0];  // (h is reused for later read-backs)
   const int64_t NE = (int64_t)h[1] - h[0] + 1;
   if (NE < 1 || (size_t)NE * nseg > kMaxFoldKeys) return FPHE_ERR_RANGE;
