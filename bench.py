@@ -11,9 +11,11 @@ with host->device and device->host copies, a decrypt round-trip check, key-holde
 encryption, ct x pt, the SecureBoost histogram (unpacked and gh-packed), the Hetero-LR
 gradient step, for N>1 the ciphertext all-gather and the cross-rank histogram fold, the
 roofline of the dominant kernel and, at N=1, the CPU baseline (libgmp port of the
-reference call sequence).
+reference call sequence).  `config5` is BASELINE config 5 in weak form: 12.5M elements per
+rank (100M at 8 GPUs), then the gather to rank 0 and the all-gather.  Progress goes to
+stderr, one line per leg; the JSON line is the only stdout.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--n ELEMENTS]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n ELEMENTS] [--config5-per-rank M]
 """
 from __future__ import annotations
 
