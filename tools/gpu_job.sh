@@ -6,6 +6,7 @@
 #       round     tests + smoke + the default bench line (args go to bench.py)
 #       bench     the default bench line only (args go to bench.py)
 #       prof      rocprofv3 --kernel-trace --stats of a short bench run
+#       profhead  the same of the headline leg alone (its stats average = the per-step kernel time)
 #       pmc       FETCH_SIZE / WRITE_SIZE passes (one counter per run): the encrypt kernel over
 #                 bench.py --n 131072, the op kernels over tools/bench_legs/ops_pmc_leg.py,
 #                 summarised into gpurun_out/TAG_pmc_encrypt27.json / TAG_pmc_ops.json
@@ -88,6 +89,18 @@ case $M in
   round) run_tests; run_smoke; run_bench "$@" ;;
   bench) run_bench "$@" ;;
   prof) run_prof "$@" ;;
+  profhead)  # kernel trace of the headline alone: every k_encrypt27<128,6> launch is a 2^20 step,
+             # so the stats' average duration is the bench's per-step kernel time
+    (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/${T}_head -o run -- python3 $R/bench.py --steps 5 --warmup 2 --no-extras --no-cpu-baseline --config5-per-rank 0 > $R/gpurun_out/${T}_head_bench.txt 2>&1) || { echo trace_failed; tail -20 gpurun_out/${T}_head_bench.txt; exit 1; }
+    grep '^{"metric"' gpurun_out/${T}_head_bench.txt | tail -1 > gpurun_out/${T}_head_bench.json
+    python3 -c "
+import csv, json
+b = json.load(open('gpurun_out/${T}_head_bench.json'))
+for r in csv.DictReader(open('gpurun_out/${T}_head/run_kernel_stats.csv')):
+    if 'k_encrypt27<128, 6>' in r['Name'] or 'k_draw_r' in r['Name'] or 'k_mont_const27<128>' in r['Name']:
+        print(r['Name'].split('(')[0][-40:], r['Calls'], round(float(r['AverageNs']) / 1e6, 3), 'ms avg')
+print('bench HIP-event kernel_ms per step', b['roofline']['kernel_ms_per_step'], 'mean', b['roofline']['kernel_ms'])
+" ;;
   pmc) run_pmc ;;
   sq) run_sq "$@" ;;
   sqhist)  # SQ / GRBM counters over tools/bench_legs/hist_leg.py ARGS (PHASES=0)
