@@ -1156,10 +1156,59 @@ fphe_status fold_level(fphe_ctx* c, FoldLevel& in, FoldOut& out, CallBufs& B, bo
   return hip_ok(hipGetLastError());
 }
 
+// every key's run of element-major items (contiguous, in.ord null) to one partial in one
+// launch: k_keytree27, a wave per key (sequential slot folds, then a product tree over the
+// wave's slots).  The outputs are compacted to the non-empty keys in key order (at most
+// in.nnz of them, the exact count on the device).
+template <int L>
+fphe_status fold_keys_tree(fphe_ctx* c, const FoldLevel& in, FoldOut& out, CallBufs& B) {
+  constexpr int TPI = L / 32, E = FPHE_WAVE / TPI, NL = rad_ll(TPI) * TPI;
+  hipStream_t s = B.s;
+  int32_t* flag = B.get<int32_t>(in.nkeys);
+  int32_t* pos = B.get<int32_t>(in.nkeys);
+  int32_t* hdr = B.get<int32_t>(4);
+  const size_t ub = in.nnz ? in.nnz : 1;
+  out.rows = B.get<u32>(ub * L);
+  out.sign = B.get<u8>(ub);
+  out.exp = B.get<int32_t>(ub);
+  out.key = B.get<int32_t>(ub);
+  if (!B.ok) return FPHE_ERR_HIP;
+  if (hipMemsetAsync(hdr, 0, 4 * sizeof(int32_t), s) != hipSuccess) return FPHE_ERR_HIP;
+  // flag[k] = (cnt[k] + 2^30 - 1) / 2^30 = 1 for a non-empty key (counts < 2^30), else 0
+  hipLaunchKernelGGL(k_gr_nchunks, dim3(gr_grid(in.nkeys, c->cus)), dim3(kGrBlock), 0, s, in.cnt, in.nkeys,
+                     (int32_t)1 << 30, flag, hdr);
+  if (dev_scan(c, flag, in.nkeys, pos, hdr + 2, B) != FPHE_OK) return FPHE_ERR_HIP;
+  int32_t* keyof = B.get<int32_t>(ub);
+  if (!B.ok) return FPHE_ERR_HIP;
+  hipLaunchKernelGGL(k_gr_keyof, dim3(gr_grid(in.nkeys, c->cus)), dim3(kGrBlock), 0, s, (const int32_t*)flag,
+                     (const int32_t*)pos, in.nkeys, keyof);
+  auto kern = KS<TPI>::template keytree<L>();
+  const size_t lds = (size_t)kWavesPerBlock * NL * E * 4;
+  set_lds(kern, lds);
+  const unsigned grid = occ_grid(c, kern, lds, ub, "keytree");  // a wave per non-empty key (bound)
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, s, c->K, in.rows, in.sign, in.exp, in.cnt, in.off,
+                     (const int32_t*)keyof, (const int32_t*)(hdr + 2), out.rows, out.sign, out.exp, out.key, (u32)NL);
+  out.cnt = flag;
+  out.off = pos;
+  out.n_dev = hdr + 2;
+  out.n_ub = ub;
+  out.maxcnt = 1;
+  return hip_ok(hipGetLastError());
+}
+
+// the largest per-key run the tree fold takes (FPHE_FOLD_TREE_MAX; 0: the chunk levels always)
+int32_t fold_tree_max() {
+  const char* e = getenv("FPHE_FOLD_TREE_MAX");
+  return e ? (int32_t)strtol(e, nullptr, 10) : 256;
+}
+
 // fold every key's run down to one partial (levels of chunked products)
 template <int L>
 fphe_status fold_runs(fphe_ctx* c, FoldLevel lv, FoldOut& out, CallBufs& B, bool read_stats) {
+  const int32_t tree_max = fold_tree_max();
   for (;;) {
+    // short runs: the rest in one tree launch (chunk levels first while runs are long)
+    if (!read_stats && !lv.ord && lv.maxcnt > 1 && lv.maxcnt <= tree_max) return fold_keys_tree<L>(c, lv, out, B);
     if (fold_level<L>(c, lv, out, B, read_stats) != FPHE_OK) return FPHE_ERR_HIP;
     read_stats = false;
     if (out.maxcnt <= 1) return FPHE_OK;

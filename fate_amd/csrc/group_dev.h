@@ -359,6 +359,14 @@ __global__ __launch_bounds__(kGrBlock) void k_gr_segcount(const int32_t* __restr
   }
 }
 
+// keyof[pos[k]] = k for every key with flag[k] set: the non-empty keys in key order
+// (k_keytree27 gives each of them its own wave)
+__global__ __launch_bounds__(kGrBlock) void k_gr_keyof(const int32_t* __restrict__ flag, const int32_t* __restrict__ pos,
+                                                       size_t nkeys, int32_t* __restrict__ keyof) {
+  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < nkeys; k += (size_t)gridDim.x * blockDim.x)
+    if (flag[k]) keyof[pos[k]] = (int32_t)k;
+}
+
 // --- chunk tables: key k's items [off[k], off[k] + cnt[k]) in chunks of klen ----------------------
 __global__ __launch_bounds__(kGrBlock) void k_gr_chunks(const int32_t* __restrict__ cnt, const int32_t* __restrict__ off,
                                                         const int32_t* __restrict__ choff, size_t nkeys, int32_t klen,
