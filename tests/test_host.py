@@ -180,3 +180,29 @@ def test_key_size_gate():
     pk = P.PK(P.keygen(512)[1].n)
     assert pk._key.L1 == 32 and pk._key.L2 == 64
     assert P.PK((1 << 3071) + 1)._key.L2 == 256
+
+
+def test_path_options_set_and_restore():
+    """fate_amd.paillier.path_options (fphe_ctx_set_option on every context; none exist on the
+    CPU): the block's settings, then the previous ones again; None means the library default;
+    an unknown name raises before anything changes."""
+    import pytest
+    from fate_amd import paillier as P
+    before_sq = P.WIDE_SQUEEZE_MAX_CHUNKS
+    before = dict(P._PATH_OPTIONS)
+    with P.path_options(**P.THROUGHPUT_PATHS, kh_direct_z=0):
+        assert P._PATH_OPTIONS[P._OPTION_IDS["wide_decrypt_max"]] == 0
+        assert P._PATH_OPTIONS[P._OPTION_IDS["kh_direct_z"]] == 0
+        assert P.WIDE_SQUEEZE_MAX_CHUNKS == 0
+        with P.path_options(wide_decrypt_max=7):
+            assert P._PATH_OPTIONS[P._OPTION_IDS["wide_decrypt_max"]] == 7
+        assert P._PATH_OPTIONS[P._OPTION_IDS["wide_decrypt_max"]] == 0
+    assert P._PATH_OPTIONS == before and P.WIDE_SQUEEZE_MAX_CHUNKS == before_sq
+    with pytest.raises(ValueError, match="unknown path option"):
+        P.set_path_options(wide_decrypt_max=1, no_such_option=3)
+    assert P._PATH_OPTIONS == before
+    # the library's enum values (include/fate_phe.h)
+    from fate_amd import _lib
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "fate_phe.h")).read()
+    for name in ("WIDE_DECRYPT_MAX", "WIDE_ENCRYPT_MAX", "WIDE_KH_ENCRYPT_MAX", "KH_DIRECT_Z"):
+        assert f"FPHE_OPT_{name} = {getattr(_lib, 'OPT_' + name)}," in hdr
