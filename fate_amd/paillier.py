@@ -1038,13 +1038,24 @@ class CiphertextVector:
         # host sync between the launches
         ferr, aerr = [], []
         folded, present = _fold_to_segments(pk, other, slot, self.count, index=src, with_present=True, deferred=ferr)
-        cur = _fit_limbs(self, pk._key.L2)
-        r = _add(pk, cur, folded, broadcast=False, deferred=aerr)
-        if _fold_failed(ferr):  # an exponent gap beyond the device merge: the exact torch path
-            folded, present = _fold_dense(pk, other, slot, self.count, src)
-            r = _add(pk, cur, folded, broadcast=False)
-        elif _fold_failed(aerr):  # a gap beyond k_add27's range: pre-aligned, exact
-            r = _add(pk, cur, folded, broadcast=False)
+        if getattr(_FRESH_ONES, "v", None) is self:
+            # a zeros() vector, the literal 1 in every slot (the operation was entered with it:
+            # _keyed): add(1, x) = x (the literal-1 rule, lib.rs:301-308, exponent and sign
+            # included), so the folded slots replace it and no ct-add runs -- SecureBoost's
+            # histograms start as zeros()
+            _resolve(self, pk.n)
+            cur = _fit_limbs(self, pk._key.L2)
+            if _fold_failed(ferr):  # an exponent gap beyond the device merge: the exact torch path
+                folded, present = _fold_dense(pk, other, slot, self.count, src)
+            r = folded
+        else:
+            cur = _fit_limbs(self, pk._key.L2)
+            r = _add(pk, cur, folded, broadcast=False, deferred=aerr)
+            if _fold_failed(ferr):  # an exponent gap beyond the device merge: the exact torch path
+                folded, present = _fold_dense(pk, other, slot, self.count, src)
+                r = _add(pk, cur, folded, broadcast=False)
+            elif _fold_failed(aerr):  # a gap beyond k_add27's range: pre-aligned, exact
+                r = _add(pk, cur, folded, broadcast=False)
         # slots no term reaches keep their value as it was (exponent of a literal 1 included:
         # the reference never touches them)
         keep = present[: r.sign.numel()] == 0
@@ -1145,6 +1156,9 @@ class CiphertextVector:
             self._assign(torch.arange(0, r.count), r)
 
 
+_FRESH_ONES = threading.local()  # .v: the in-place target known to hold only literal 1s (_keyed)
+
+
 def _keyed(fn):
     """Stamp the key's modulus on the vectors an operation returns (and on an in-place
     target that had none, e.g. a ``zeros()`` histogram): from its PK argument, else from
@@ -1154,9 +1168,17 @@ def _keyed(fn):
     @functools.wraps(fn)
     def w(self, *args, **kw):
         pk = next((a for a in itertools.chain(args, kw.values()) if isinstance(a, PK)), None)
+        # an in-place target that is still a zeros() vector (the literal 1 everywhere) for the
+        # length of this call only: _fold_terms then replaces its slots instead of adding
+        fresh = isinstance(self, CiphertextVector) and self.raw and self.lit
         if pk is not None:  # unpickled operands get their key before any arithmetic
             _resolve_args(pk.n, self, *args, *kw.values())
-        r = fn(self, *args, **kw)
+        prev = getattr(_FRESH_ONES, "v", None)
+        _FRESH_ONES.v = self if fresh else None
+        try:
+            r = fn(self, *args, **kw)
+        finally:
+            _FRESH_ONES.v = prev
         n = pk.n if pk is not None else self.n
         if n is not None and not self.raw:
             if self.n is None:
