@@ -456,3 +456,32 @@ def test_empty_and_degenerate_vector_ops(env):
     got = dev_vec(pk, []).rmatmul(pk, pv0, [0, 3], [2, 0])
     assert host(pk, got) == ref(O.rmatmul(opk, [], [], [0, 3], [2, 0]))
     assert sk.decrypt_to_encoded(empty).to_ints() == ([], [])
+
+
+def test_iupdate_into_fresh_zeros(env):
+    """iupdate / iupdate_with_masks into a zeros() histogram take the literal-1 fast path (the
+    folded slots replace the literal 1s, add(1, x) = x, lib.rs:301-308); the result equals the
+    reference's sequential loop from zeros, untouched slots keep the literal 1 with exp 0, and
+    a second iupdate into the same (now non-zero) vector adds as usual."""
+    fx, sk, pk, coder, opk, cts = env
+    rng = random.Random(11)
+    stride = 2
+    cts = more(opk, cts, 60)
+    other = cts[:20 * stride]
+    other[5] = O.ct_zero()  # a literal-1 term
+    indexes = [[rng.randrange(7) for _ in range(rng.randrange(0, 3))] for _ in range(20)]
+    v = P.CiphertextVector.zeros(10 * stride, pk._key.L2)  # slots 7..9 get no terms
+    v.iupdate(dev_vec(pk, other), indexes, stride, pk)
+    want = [O.ct_zero() for _ in range(10 * stride)]
+    O.iupdate(opk, want, other, indexes, stride)
+    assert host(pk, v) == ref(want)
+    v.iupdate(dev_vec(pk, other), indexes, stride, pk)  # no longer zeros: the ct-add path
+    O.iupdate(opk, want, other, indexes, stride)
+    assert host(pk, v) == ref(want)
+    masks = [rng.random() < 0.6 for _ in range(20)]
+    idx2 = [[rng.randrange(10)] for _ in range(sum(masks))]
+    v2 = P.CiphertextVector.zeros(10 * stride, pk._key.L2)
+    v2.iupdate_with_masks(dev_vec(pk, other), idx2, masks, stride, pk)
+    want2 = [O.ct_zero() for _ in range(10 * stride)]
+    O.iupdate_with_masks(opk, want2, other, idx2, masks, stride)
+    assert host(pk, v2) == ref(want2)
