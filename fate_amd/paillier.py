@@ -1045,8 +1045,14 @@ class CiphertextVector:
             # histograms start as zeros()
             _resolve(self, pk.n)
             cur = _fit_limbs(self, pk._key.L2)
-            if _fold_failed(ferr):  # an exponent gap beyond the device merge: the exact torch path
-                folded, present = _fold_dense(pk, other, slot, self.count, src)
+            if not _fold_failed(ferr):
+                # fphe_fold_segments already wrote the literal 1 (M(1), sign 0, exp 0) into every
+                # segment no term reaches -- what cur holds there -- so the fold is the result
+                self.C, self.sign, self.exp = folded.C, folded.sign, folded.exp
+                self.ebound = _ebound_union(cur.ebound, other.ebound)
+                return
+            # an exponent gap beyond the device merge: the exact torch path
+            folded, present = _fold_dense(pk, other, slot, self.count, src)
             r = folded
         else:
             cur = _fit_limbs(self, pk._key.L2)
