@@ -719,18 +719,36 @@ __global__ __launch_bounds__(kGrBlock) void k_gr_gapkeys(const int32_t* __restri
 
 // --- element-major <-> tile-major ------------------------------------------------------------------
 // One block per 64-element tile: [L][64] words (coalesced 256-B rows) -> 64 rows of L words
-// (coalesced), through LDS with a 65-word row pitch (no bank conflicts on the transposed read).
+// (coalesced), through LDS with a 65-word row pitch.  Global loads and stores are 16 bytes a
+// lane (a tile's L*64/4 of them issued before the first LDS write); the transposed LDS read
+// of four limbs of one element is at most 2-way bank-conflicted at that pitch.
 template <int L>
 __global__ __launch_bounds__(kGrBlock) void k_tiles_to_rows(const u32* __restrict__ C, size_t count, u32* __restrict__ rows) {
+  static_assert((L * FPHE_WAVE / 4) % kGrBlock == 0 && L % 4 == 0, "whole 16-byte vectors per thread");
+  constexpr int kV = L * FPHE_WAVE / 4, kPer = kV / kGrBlock, kRowV = L / 4;
   __shared__ u32 t[L][FPHE_WAVE + 1];
   const size_t ntiles = (count + FPHE_WAVE - 1) / FPHE_WAVE;
   for (size_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const u32* src = C + tile * L * FPHE_WAVE;
-    for (int i = threadIdx.x; i < L * FPHE_WAVE; i += kGrBlock) t[i >> 6][i & 63] = src[i];
+    const uint4* src = reinterpret_cast<const uint4*>(C + tile * L * FPHE_WAVE);
+    uint4 v[kPer];
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) v[r] = src[threadIdx.x + r * kGrBlock];
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+      const int i = threadIdx.x + r * kGrBlock, j = i >> 4, c = (i & 15) * 4;
+      t[j][c] = v[r].x;
+      t[j][c + 1] = v[r].y;
+      t[j][c + 2] = v[r].z;
+      t[j][c + 3] = v[r].w;
+    }
     __syncthreads();
     const size_t e0 = tile * FPHE_WAVE;
     const int ne = count - e0 < (size_t)FPHE_WAVE ? (int)(count - e0) : FPHE_WAVE;
-    for (int i = threadIdx.x; i < ne * L; i += kGrBlock) rows[(e0 + i / L) * L + i % L] = t[i % L][i / L];
+    uint4* dst = reinterpret_cast<uint4*>(rows + e0 * L);
+    for (int i = threadIdx.x; i < ne * kRowV; i += kGrBlock) {
+      const int e = i / kRowV, k = (i % kRowV) * 4;
+      dst[i] = make_uint4(t[k][e], t[k + 1][e], t[k + 2][e], t[k + 3][e]);
+    }
     __syncthreads();
   }
 }

@@ -1040,18 +1040,20 @@ class CiphertextVector:
         folded, present = _fold_to_segments(pk, other, slot, self.count, index=src, with_present=True, deferred=ferr)
         if getattr(_FRESH_ONES, "v", None) is self:
             # a zeros() vector, the literal 1 in every slot (the operation was entered with it:
-            # _keyed): add(1, x) = x (the literal-1 rule, lib.rs:301-308, exponent and sign
-            # included), so the folded slots replace it and no ct-add runs -- SecureBoost's
-            # histograms start as zeros()
-            _resolve(self, pk.n)
-            cur = _fit_limbs(self, pk._key.L2)
+            # _keyed, which leaves it key-less): add(1, x) = x (the literal-1 rule,
+            # lib.rs:301-308, exponent and sign included), so the folded slots replace it and no
+            # ct-add runs -- SecureBoost's histograms start as zeros()
             if not _fold_failed(ferr):
                 # fphe_fold_segments already wrote the literal 1 (M(1), sign 0, exp 0) into every
-                # segment no term reaches -- what cur holds there -- so the fold is the result
+                # segment no term reaches -- what the vector holds there -- so the fold is the
+                # result, and the vector takes the key with it (no M(1) fill first)
                 self.C, self.sign, self.exp = folded.C, folded.sign, folded.exp
-                self.ebound = _ebound_union(cur.ebound, other.ebound)
+                self.n, self.raw, self.lit = pk.n, False, False
+                self.ebound = _ebound_union(self.ebound, other.ebound)
                 return
             # an exponent gap beyond the device merge: the exact torch path
+            _resolve(self, pk.n)
+            cur = _fit_limbs(self, pk._key.L2)
             folded, present = _fold_dense(pk, other, slot, self.count, src)
             r = folded
         else:
@@ -1163,6 +1165,9 @@ class CiphertextVector:
 
 
 _FRESH_ONES = threading.local()  # .v: the in-place target known to hold only literal 1s (_keyed)
+# the in-place methods whose fold replaces a zeros() target (_fold_terms): _keyed leaves such a
+# target key-less on entry, so its M(1) fill is never made only to be replaced
+_FRESH_TARGETS = frozenset({"iupdate", "iupdate_with_masks"})
 
 
 def _keyed(fn):
@@ -1178,7 +1183,10 @@ def _keyed(fn):
         # length of this call only: _fold_terms then replaces its slots instead of adding
         fresh = isinstance(self, CiphertextVector) and self.raw and self.lit
         if pk is not None:  # unpickled operands get their key before any arithmetic
-            _resolve_args(pk.n, self, *args, *kw.values())
+            if fresh and fn.__name__ in _FRESH_TARGETS:
+                _resolve_args(pk.n, *args, *kw.values())
+            else:
+                _resolve_args(pk.n, self, *args, *kw.values())
         prev = getattr(_FRESH_ONES, "v", None)
         _FRESH_ONES.v = self if fresh else None
         try:
@@ -1515,9 +1523,13 @@ def _fold_to_segments(pk: "PK", src: CiphertextVector, seg: torch.Tensor, nseg: 
     idx = None if index is None else index.to(dev, torch.int32).contiguous()
     if idx is not None and idx.numel() != T:
         raise ValueError("fold: index and segment arrays differ in length")
-    out = CiphertextVector.empty(nseg, L2, dev)
-    out.n = pk.n
-    present = torch.zeros(_ntiles(nseg) * WAVE, dtype=torch.uint8, device=dev)
+    # fphe_fold_segments writes every word of these first (k_gr_init_out: the literal 1, exp 0,
+    # not present, tile padding included), so none is zeroed here
+    nt = _ntiles(nseg)
+    out = CiphertextVector(torch.empty((nt, L2, WAVE), dtype=torch.int32, device=dev),
+                           torch.empty(nt * WAVE, dtype=torch.uint8, device=dev),
+                           torch.empty(nt * WAVE, dtype=torch.int32, device=dev), nseg, pk.n)
+    present = torch.empty(nt * WAVE, dtype=torch.uint8, device=dev)
     if nseg == 0:
         if T:
             raise PanicException("index out of bounds")

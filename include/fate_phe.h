@@ -267,7 +267,8 @@ fphe_status fphe_fold(fphe_ctx* ctx, const uint32_t* Src, const uint8_t* ssign, 
  * entries.  Outputs are tile-major [ceil(nseg/64)] vectors: a segment without terms gets the
  * reference's zero (the literal 1, exp 0) and present[s] = 0 (present may be NULL); a segment
  * whose fold is the literal 1 takes the exponent of its last term, as the sequential fold.
- * Terms are counting-sorted by (segment, exponent) on the device, each run folded by chunked
+ * Every word of Co, so, eo and present (tile padding included) is written before any term is
+ * read, so the caller need not initialise them.  Terms are counting-sorted by (segment, exponent) on the device, each run folded by chunked
  * Montgomery products, every segment's per-exponent partials aligned to its least exponent and
  * folded.  FPHE_ERR_ARG for an index or segment out of range; FPHE_ERR_RANGE when nseg x the
  * exponent range exceeds 2^25 buckets.  Synchronises the stream a few times (sizes). */
