@@ -16,7 +16,8 @@
 #endif
 #define FPHE_OCC2 __attribute__((amdgpu_waves_per_eu(2)))
 // ct-add / ct x pt / squeeze run at 3 waves too (same-box A/B, profiles/r02/
-// r02f_ab_occ3_ops.txt: add +5%, ct x pt +1%); the segmented fold stays at 2 (-7% at 3).
+// r02f_ab_occ3_ops.txt: add +5%, ct x pt +1%); the segmented fold stays at 2 (-7% at 3;
+// again -7% in round 6 with 308 B/lane spilled, profiles/r06/r06x_ab_fold_occ3_negative.txt).
 // Round 1's 3-wave k_add27<64> memory fault was the register allocator reusing a
 // per-lane buffer descriptor's VGPRs for a spill reload inside the readfirstlane loop
 // the compiler builds around such a load; the kernels no longer pick a
