@@ -213,6 +213,33 @@ def test_iupdate_and_masks(env):
     assert host(pk, v2) == ref(want2)
 
 
+def test_iupdate_fresh_zeros_target_edges(env):
+    """The zeros() target stays key-less until the fold hands it the key (_keyed leaves it so
+    for iupdate / iupdate_with_masks): a panicking call, a call with no terms and a [samples,
+    positions] tensor call must leave it exactly the reference's value, and a zeros() vector
+    folded into itself reads literal-1 terms (lib.rs:301-308, 724-747)."""
+    fx, sk, pk, coder, opk, cts = env
+    stride = 2
+    cts = more(opk, cts, 40, seed=3)
+    other = cts[:12 * stride]
+    v = P.CiphertextVector.zeros(6 * stride, pk._key.L2)
+    with pytest.raises(P.PanicException):  # position 6 is past 12 / 2 slots
+        v.iupdate(dev_vec(pk, other), [[0], [6]] + [[] for _ in range(10)], stride, pk)
+    v.iupdate(dev_vec(pk, other), [[] for _ in range(12)], stride, pk)  # no terms at all
+    want = [O.ct_zero() for _ in range(6 * stride)]
+    assert host(pk, v) == ref(want)
+    pos = torch.tensor([[(3 * i) % 6, (i + 1) % 6] for i in range(12)], dtype=torch.int64)
+    v.iupdate(dev_vec(pk, other), pos.to(v.device), stride, pk)
+    O.iupdate(opk, want, other, pos.tolist(), stride)
+    assert host(pk, v) == ref(want)
+    # a zeros() vector as its own source: every term is the literal 1
+    z = P.CiphertextVector.zeros(4 * stride, pk._key.L2)
+    z.iupdate(z, [[1], [1, 3]], stride, pk)
+    wz = [O.ct_zero() for _ in range(4 * stride)]
+    O.iupdate(opk, wz, [O.ct_zero() for _ in range(4 * stride)], [[1], [1, 3]], stride)
+    assert host(pk, z) == ref(wz)
+
+
 def _fold_terms(opk, count, seed):
     """Terms for the segmented fold: long equal-exponent runs (> 64, several fphe_fold
     rounds), negative ciphertext integers (sign 1), other exponents, literal 1s with
