@@ -954,7 +954,17 @@ def main() -> None:
         hist_h.iupdate(gh, positions, 2, pk)  # positions as a host tensor: + the H2D copy
         torch.cuda.synchronize(dev)
         hist_host_s = time.perf_counter() - t0h
-        del hist_h
+        # positions as the reference's caller hands them over: Vec<Vec<usize>>, one Python list per
+        # sample (HistogramIndexer.get_positions, arch/histogram/_histogram_local.py:68-82), read
+        # by the host helper; the lists are made before the clock starts
+        pos_lists = positions.tolist()
+        hist_h = P.CiphertextVector.zeros(HF * NB * 2, pk._key.L2, dev)
+        torch.cuda.synchronize(dev)
+        t0h = time.perf_counter()
+        hist_h.iupdate(gh, pos_lists, 2, pk)
+        torch.cuda.synchronize(dev)
+        hist_list_s = time.perf_counter() - t0h
+        del hist_h, pos_lists
         iupdate_block = iupdate_roofline(gh, positions, 2, HF * NB * 2, hist_s, key_bits)
         iupdate_block.update(at_clock(iupdate_block["frac"], hist_clock[0]))
         # the same call 5 times back to back (no host sync between calls; each still reads
@@ -1102,6 +1112,7 @@ def main() -> None:
             "histogram_scatter_adds_per_s": round(N * HF * 2 / hist_s, 1),
             "histogram_iupdate_s": round(hist_s, 5),
             "histogram_iupdate_host_positions_s": round(hist_host_s, 5),
+            "histogram_iupdate_list_positions_s": round(hist_list_s, 5),
             "histogram_edge_values": hist_edge,
             "histogram_config": f"{N} samples x {HF} features x {NB} bins x (g,h), SecureBoost-shaped g = p - y, "
                                 f"h = p(1 - p) (key-holder encryptions, untimed), iupdate fold on device",

@@ -161,6 +161,30 @@ def load() -> ctypes.CDLL:
         return lib
 
 
+# host helper (fate_amd/csrc/host_positions.c): CPython-API marshalling of position lists,
+# called with the GIL held (ctypes.PyDLL), no device code
+PY_LIB_PATH = os.path.join(_HERE, "lib", "libfphe_py.so")
+_pylib: Optional[ctypes.PyDLL] = None
+
+
+def load_py() -> ctypes.PyDLL:
+    """Load (once) the host helper library.  Raises NativeLibraryMissing."""
+    global _pylib
+    with _lock:
+        if _pylib is not None:
+            return _pylib
+        if not os.path.exists(PY_LIB_PATH):
+            raise NativeLibraryMissing(
+                f"{PY_LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+        lib = ctypes.PyDLL(PY_LIB_PATH)
+        lib.fphe_py_positions_lens.argtypes = [ctypes.py_object, vp]
+        lib.fphe_py_positions_lens.restype = ctypes.c_int64
+        lib.fphe_py_positions_fill.argtypes = [ctypes.py_object, vp, ctypes.c_int64]
+        lib.fphe_py_positions_fill.restype = ctypes.c_int64
+        _pylib = lib
+        return lib
+
+
 def check(status: int, what: str) -> None:
     if status == FPHE_OK:
         return

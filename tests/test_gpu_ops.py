@@ -232,6 +232,16 @@ def test_iupdate_fresh_zeros_target_edges(env):
     v.iupdate(dev_vec(pk, other), pos.to(v.device), stride, pk)
     O.iupdate(opk, want, other, pos.tolist(), stride)
     assert host(pk, v) == ref(want)
+    # the same positions as rectangular lists (one per sample: the tensor path) and as a numpy
+    # matrix, into a zeros() target and into a vector that already holds sums
+    for form in (pos.tolist(), pos.numpy()):
+        w = P.CiphertextVector.zeros(6 * stride, pk._key.L2)
+        w.iupdate(dev_vec(pk, other), form, stride, pk)
+        w.iupdate(dev_vec(pk, other), form, stride, pk)
+        w2 = [O.ct_zero() for _ in range(6 * stride)]
+        O.iupdate(opk, w2, other, pos.tolist(), stride)
+        O.iupdate(opk, w2, other, pos.tolist(), stride)
+        assert host(pk, w) == ref(w2)
     # a zeros() vector as its own source: every term is the literal 1
     z = P.CiphertextVector.zeros(4 * stride, pk._key.L2)
     z.iupdate(z, [[1], [1, 3]], stride, pk)

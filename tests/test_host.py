@@ -206,3 +206,33 @@ def test_path_options_set_and_restore():
     hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "fate_phe.h")).read()
     for name in ("WIDE_DECRYPT_MAX", "WIDE_ENCRYPT_MAX", "WIDE_KH_ENCRYPT_MAX", "KH_DIRECT_Z"):
         assert f"FPHE_OPT_{name} = {getattr(_lib, 'OPT_' + name)}," in hdr
+
+
+def test_position_lists_host_helper():
+    """The reference's Vec<Vec<usize>> position lists (paillier.rs:261-283) read by the CPython
+    helper (fate_amd/csrc/host_positions.c): same order as walking them in Python, ragged and
+    empty lists, tuples, numpy integers and iterables; a non-integer position is a TypeError
+    (pyo3's usize extraction), a non-sequence sample likewise."""
+    import itertools
+    import random
+
+    from fate_amd import paillier as P
+    rng = random.Random(3)
+    lists = [[rng.randrange(1 << 20) for _ in range(rng.randrange(0, 5))] for _ in range(2000)]
+    lists[7] = (3, 1, 2)
+    lists[8] = [np.int64(5), np.int32(9)]
+    lens, pos = P._position_lists(lists)
+    assert lens.tolist() == [len(x) for x in lists]
+    assert pos.tolist() == [int(v) for v in itertools.chain.from_iterable(lists)]
+    lens, pos = P._position_lists(iter([[1, 2], [], [3]]))
+    assert lens.tolist() == [2, 0, 1] and pos.tolist() == [1, 2, 3]
+    lens, pos = P._position_lists([])
+    assert lens.size == 0 and pos.size == 0
+    ii, pp = P._flatten_positions([[4], [], [5, 6]], None)
+    assert ii.tolist() == [0, 2, 2] and pp.tolist() == [4, 5, 6]
+    with pytest.raises(TypeError):
+        P._position_lists([[1, 2.5]])
+    with pytest.raises(TypeError):
+        P._position_lists([[1], 7])
+    with pytest.raises(OverflowError):
+        P._position_lists([[1 << 70]])
