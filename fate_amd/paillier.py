@@ -1006,7 +1006,12 @@ class CiphertextVector:
     def iupdate_with_masks(self, other: "CiphertextVector", indexes, masks, stride: int, pk: "PK") -> None:
         """``CiphertextVector::iupdate_with_masks`` (lib.rs:736-747): the k-th position list
         belongs to the k-th sample whose mask is true."""
-        m = torch.as_tensor(list(masks) if not isinstance(masks, torch.Tensor) else masks, dtype=torch.bool)
+        if isinstance(masks, torch.Tensor):
+            m = masks.to(torch.bool)
+        elif isinstance(masks, np.ndarray):
+            m = torch.from_numpy(masks.astype(bool, copy=False).reshape(-1))
+        else:  # Vec<bool>: a Python list, read in C by numpy (3x a tensor from the list)
+            m = torch.from_numpy(np.fromiter(masks, dtype=bool))
         vpos = torch.nonzero(m.to(self.device)).squeeze(1).to(torch.int32)
         ii, pp = _flatten_positions(indexes, self.device)
         if ii.numel():
