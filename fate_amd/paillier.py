@@ -814,13 +814,19 @@ class CiphertextVector:
         self.lit = False
 
     def intervals_slice(self, intervals: Sequence[Tuple[int, int]]) -> "CiphertextVector":
-        """``CiphertextVector::intervals_slice`` (lib.rs:499-513)."""
-        parts = []
-        for s, e in intervals:
-            if e > self.count:
-                raise RuntimeError(f"end index out of range: start={s}, end={e}, data_size={self.count}")
-            parts.append(torch.arange(s, e))
-        idx = torch.cat(parts) if parts else torch.zeros(0, dtype=torch.long)
+        """``CiphertextVector::intervals_slice`` (lib.rs:499-513): the intervals' elements, in
+        order.  The first interval that fails decides the error, as the reference's loop: an end
+        past the data is its anyhow error (RuntimeError), a start past the end the slice panic."""
+        s, e = _interval_array(intervals)
+        n = self.count
+        bad = torch.nonzero((e > n) | (s > e)).squeeze(1)
+        if bad.numel():
+            i = int(bad[0])
+            si, ei = int(s[i]), int(e[i])
+            if ei > n:
+                raise RuntimeError(f"end index out of range: start={si}, end={ei}, data_size={n}")
+            raise PanicException(f"slice index starts at {si} but ends at {ei}")
+        idx, _ = _interval_items(s, e)
         return self._gather(idx)
 
     def tolist(self) -> List["CiphertextVector"]:
@@ -1117,17 +1123,22 @@ class CiphertextVector:
                                 ) -> "CiphertextVector":
         """``CiphertextVector::intervals_sum_with_step`` (lib.rs:773-788): out[i*step + c] =
         fold of data[s+k] over k = c (mod step), s+k < e, from zero."""
-        idx, seg = [], []
-        for i, (s_, e_) in enumerate(intervals):
-            if e_ > self.count or s_ > e_:
-                raise PanicException(f"range end index {e_} out of range for slice of length {self.count}")
-            k = torch.arange(s_, e_)
-            idx.append(k)
-            seg.append(i * step + (k - s_) % step)
-        nout = len(intervals) * step
-        if not idx or sum(k.numel() for k in idx) == 0:
+        s, e = _interval_array(intervals)
+        n = self.count
+        bad = torch.nonzero((e > n) | (s > e)).squeeze(1)
+        if bad.numel():  # &self.data[s..e] of the first failing interval (lib.rs:781)
+            i = int(bad[0])
+            si, ei = int(s[i]), int(e[i])
+            if si > ei:
+                raise PanicException(f"slice index starts at {si} but ends at {ei}")
+            raise PanicException(f"range end index {ei} out of range for slice of length {n}")
+        step = int(step)
+        nout = s.numel() * step
+        idx, rel = _interval_items(s, e)
+        if idx.numel() == 0 or step == 0:  # step 0: empty chunks, (0..0).cycle() adds nothing
             return CiphertextVector.zeros(nout, self.L2, self.device)
-        return _fold_to_segments(pk, self, torch.cat(seg), nout, index=torch.cat(idx))
+        seg = torch.repeat_interleave(torch.arange(s.numel(), dtype=torch.int64) * step, e - s) + rel % step
+        return _fold_to_segments(pk, self, seg, nout, index=idx)
 
     def pack_squeeze(self, pack_num: int, offset_bit: int, pk: "PK") -> "CiphertextVector":
         """``CiphertextVector::pack_squeeze`` (paillier.rs:241; lib.rs:439-450): per chunk of
@@ -1405,6 +1416,27 @@ def _flatten_positions(indexes, dev=None) -> Tuple[torch.Tensor, torch.Tensor]:
     lens, pos = _position_lists(indexes)
     ii = torch.from_numpy(np.repeat(np.arange(lens.size, dtype=np.int64), lens))
     return ii.to(dev), torch.from_numpy(pos).to(dev)
+
+
+def _interval_array(intervals) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Vec<(usize, usize)> as (starts, ends) int64 tensors; a negative bound is pyo3's usize
+    extraction error."""
+    iv = torch.tensor([(int(a), int(b)) for a, b in intervals], dtype=torch.int64).reshape(-1, 2)
+    if iv.numel() and bool((iv < 0).any()):
+        raise OverflowError("can't convert negative int to unsigned")
+    return iv[:, 0], iv[:, 1]
+
+
+def _interval_items(s: torch.Tensor, e: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """The element indexes of consecutive intervals [s_i, e_i) (s <= e), concatenated, and each
+    one's offset inside its interval."""
+    lens = e - s
+    total = int(lens.sum()) if lens.numel() else 0
+    if total == 0:
+        z = torch.zeros(0, dtype=torch.int64)
+        return z, z
+    rel = torch.arange(total, dtype=torch.int64) - torch.repeat_interleave(torch.cumsum(lens, 0) - lens, lens)
+    return torch.repeat_interleave(s, lens) + rel, rel
 
 
 def _position_lists(indexes) -> Tuple[np.ndarray, np.ndarray]:

@@ -345,6 +345,22 @@ def test_intervals_sum_with_step(env):
     intervals, step = [(0, 7), (7, 7), (10, 30)], 3
     got = dev_vec(pk, data).intervals_sum_with_step(pk, intervals, step)
     assert host(pk, got) == ref(O.intervals_sum_with_step(opk, data, intervals, step))
+    # many overlapping intervals (a histogram's node x feature ranges), and intervals_slice
+    rng = random.Random(4)
+    many = []
+    for _ in range(300):
+        a = rng.randrange(30)
+        many.append((a, rng.randrange(a, 31)))
+    got = dev_vec(pk, data).intervals_sum_with_step(pk, many, 2)
+    assert host(pk, got) == ref(O.intervals_sum_with_step(opk, data, many, 2))
+    got = dev_vec(pk, data).intervals_slice(many)
+    assert host(pk, got) == ref([x for a, b in many for x in data[a:b]])
+    # step 0: empty chunks (the reference's (0..0).cycle() adds nothing), the ranges still checked
+    assert host(pk, dev_vec(pk, data).intervals_sum_with_step(pk, intervals, 0)) == []
+    with pytest.raises(P.PanicException, match="slice index starts at 9 but ends at 8"):
+        dev_vec(pk, data).intervals_sum_with_step(pk, [(0, 3), (9, 8), (0, 31)], 2)
+    with pytest.raises(P.PanicException, match="range end index 31 out of range for slice of length 30"):
+        dev_vec(pk, data).intervals_sum_with_step(pk, [(0, 3), (0, 31), (9, 8)], 0)
 
 
 def test_matmul_rmatmul(env):

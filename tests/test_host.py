@@ -236,3 +236,22 @@ def test_position_lists_host_helper():
         P._position_lists([[1], 7])
     with pytest.raises(OverflowError):
         P._position_lists([[1 << 70]])
+
+
+def test_interval_bounds_follow_the_reference():
+    """intervals_slice's checks in the reference's order (lib.rs:499-513): the first failing
+    interval decides; an end past the data is the anyhow error (RuntimeError), a start past its
+    end the slice panic; a negative bound is pyo3's usize error.  Checked before any device
+    work, so a CPU-resident vector shows them."""
+    from fate_amd import paillier as P
+    v = P.CiphertextVector(torch.zeros((1, 128, 64), dtype=torch.int32), torch.zeros(64, dtype=torch.uint8),
+                           torch.zeros(64, dtype=torch.int32), 10)
+    with pytest.raises(RuntimeError, match="end index out of range: start=3, end=11, data_size=10"):
+        v.intervals_slice([(0, 2), (3, 11), (5, 4)])
+    with pytest.raises(P.PanicException, match="slice index starts at 5 but ends at 4"):
+        v.intervals_slice([(0, 2), (5, 4), (3, 11)])
+    with pytest.raises(OverflowError):
+        v.intervals_slice([(-1, 2)])
+    s, e = P._interval_array([(2, 5), (0, 0), (7, 9)])
+    idx, rel = P._interval_items(s, e)
+    assert idx.tolist() == [2, 3, 4, 7, 8] and rel.tolist() == [0, 1, 2, 0, 1]
