@@ -161,8 +161,8 @@ def load() -> ctypes.CDLL:
         return lib
 
 
-# host helper (fate_amd/csrc/host_positions.c): CPython-API marshalling of position lists,
-# called with the GIL held (ctypes.PyDLL), no device code
+# host helper (fate_amd/csrc/host_positions.c): CPython-API marshalling of position lists and
+# i_shuffle's cycle walk, called with the GIL held (ctypes.PyDLL), no device code
 PY_LIB_PATH = os.path.join(_HERE, "lib", "libfphe_py.so")
 _pylib: Optional[ctypes.PyDLL] = None
 
@@ -181,6 +181,8 @@ def load_py() -> ctypes.PyDLL:
         lib.fphe_py_positions_lens.restype = ctypes.c_int64
         lib.fphe_py_positions_fill.argtypes = [ctypes.py_object, vp, ctypes.c_int64]
         lib.fphe_py_positions_fill.restype = ctypes.c_int64
+        lib.fphe_cycle_walk.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, vp, vp, vp]
+        lib.fphe_cycle_walk.restype = ctypes.c_int
         _pylib = lib
         return lib
 

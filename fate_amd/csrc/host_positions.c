@@ -1,4 +1,6 @@
-/* Host-side marshalling of the reference's position lists for CiphertextVector::iupdate /
+/* Host-side index work of the vector ops (no device code; loaded through ctypes.PyDLL).
+ *
+ * 1. Marshalling of the reference's position lists for CiphertextVector::iupdate /
  * iupdate_with_masks (fixedpoint_paillier/src/lib.rs:724-747; paillier.rs:261-283 takes them
  * as Vec<Vec<usize>>, which pyo3 extracts element by element).  SecureBoost hands them over
  * as Python lists of lists (HistogramIndexer.get_positions, arch/histogram/
@@ -71,4 +73,49 @@ int64_t fphe_py_positions_fill(PyObject* outer, int64_t* pos, int64_t total) {
     return -1;
   }
   return total;
+}
+
+/* 2. CiphertextVector::i_shuffle's cycle walk (fixedpoint_paillier/src/lib.rs:473-490) on
+ * positions instead of ciphertexts: perm[k] = the original element that ends at k, so the
+ * device does one gather.  The walk is the reference's, swap for swap, so any index list --
+ * not only a permutation -- gives the reference's result.  Returns 0, or 1 at the first
+ * access the reference would panic on, with bad[0] = the length indexed and bad[1] = the
+ * index ("index out of bounds: the len is .. but the index is .."): indexes[i] past the list
+ * (nix < n), or visited[next] past the data.  Indexes are non-negative (usize). */
+int fphe_cycle_walk(const int64_t* ix, int64_t nix, int64_t n, int64_t* perm, uint8_t* visited, int64_t* bad) {
+  for (int64_t k = 0; k < n; ++k) {
+    perm[k] = k;
+    visited[k] = 0;
+  }
+  for (int64_t i = 0; i < n; ++i) {
+    if (visited[i]) continue;
+    if (i >= nix) {
+      bad[0] = nix;
+      bad[1] = i;
+      return 1;
+    }
+    if (ix[i] == i) continue;
+    int64_t current = i, next = ix[current];
+    for (;;) {
+      if (next >= n) {
+        bad[0] = n;
+        bad[1] = next;
+        return 1;
+      }
+      if (visited[next] || next == i) break;
+      const int64_t t = perm[current];
+      perm[current] = perm[next];
+      perm[next] = t;
+      visited[current] = 1;
+      current = next;
+      if (current >= nix) {
+        bad[0] = nix;
+        bad[1] = current;
+        return 1;
+      }
+      next = ix[current];
+    }
+    visited[current] = 1;
+  }
+  return 0;
 }

@@ -81,12 +81,43 @@ def _permute(C_in, s_in, e_in, L: int, idx: torch.Tensor, nspace: int, scatter: 
                                             ctypes.c_void_p(_stream(dev))), "fphe_permute")
 
 
-def _check_indexes(idx: Sequence[int], n: int) -> None:
-    """The reference indexes a Vec: an index outside [0, n) panics (slice_indexes,
-    i_shuffle: fixedpoint_paillier/src/lib.rs:457-490)."""
-    bad = [i for i in idx if not 0 <= int(i) < n]
-    if bad:
-        raise PanicException(f"index out of bounds: the len is {n} but the index is {bad[0]}")
+def _index_array(indexes) -> np.ndarray:
+    """Vec<usize> (a list, tuple, array or tensor of integers) as an int64 array; a negative
+    index is pyo3's usize extraction error."""
+    if isinstance(indexes, torch.Tensor):
+        a = indexes.detach().cpu().numpy()
+    else:
+        a = np.asarray(indexes if isinstance(indexes, (list, tuple, np.ndarray)) else list(indexes))
+    if a.size == 0:
+        return np.zeros(0, dtype=np.int64)
+    if a.dtype == np.bool_ or not np.issubdtype(a.dtype, np.integer):
+        raise TypeError("indexes must be integers")
+    a = a.astype(np.int64, copy=False).reshape(-1)
+    if bool((a < 0).any()):
+        raise OverflowError("can't convert negative int to unsigned")
+    return a
+
+
+def _check_indexes(idx: np.ndarray, n: int) -> None:
+    """The reference indexes a Vec: the first index outside [0, n) panics (slice_indexes,
+    fixedpoint_paillier/src/lib.rs:457-463)."""
+    bad = np.flatnonzero(idx >= n)
+    if bad.size:
+        raise PanicException(f"index out of bounds: the len is {n} but the index is {int(idx[bad[0]])}")
+
+
+def _cycle_walk(idx: np.ndarray, n: int) -> np.ndarray:
+    """CiphertextVector::i_shuffle's swaps (lib.rs:473-490) replayed on positions by the host
+    helper: perm[k] = the element that ends at k; the reference's first out-of-bounds access
+    panics with its message."""
+    idx = np.ascontiguousarray(idx, dtype=np.int64)
+    perm = np.empty(n, dtype=np.int64)
+    visited = np.empty(n, dtype=np.uint8)
+    bad = np.zeros(2, dtype=np.int64)
+    if _lib.load_py().fphe_cycle_walk(idx.ctypes.data, idx.size, n, perm.ctypes.data, visited.ctypes.data,
+                                      bad.ctypes.data):
+        raise PanicException(f"index out of bounds: the len is {int(bad[0])} but the index is {int(bad[1])}")
+    return perm
 
 
 # --------------------------------------------------------------------------------------
@@ -788,9 +819,9 @@ class CiphertextVector:
 
     def slice_indexes(self, indexes: Sequence[int]) -> "CiphertextVector":
         """``CiphertextVector::slice_indexes`` (lib.rs:457-463)."""
-        indexes = list(indexes)
-        _check_indexes(indexes, self.count)
-        return self._gather(torch.as_tensor(indexes, dtype=torch.long))
+        idx = _index_array(indexes)
+        _check_indexes(idx, self.count)
+        return self._gather(torch.from_numpy(idx))
 
     def cat(self, others: Sequence["CiphertextVector"]) -> "CiphertextVector":
         """``CiphertextVector::cat`` (lib.rs:465-471)."""
@@ -804,12 +835,12 @@ class CiphertextVector:
         return out
 
     def i_shuffle(self, indexes: Sequence[int]) -> None:
-        """``CiphertextVector::i_shuffle`` (lib.rs:473-490).  The cycle walk permutes
-        data so that new[i] = old[indexes[i]] when ``indexes`` is a permutation."""
-        indexes = list(indexes)
-        _check_indexes(indexes, self.count)
-        idx = torch.as_tensor(indexes, dtype=torch.long)
-        g = self._gather(idx)
+        """``CiphertextVector::i_shuffle`` (lib.rs:473-490).  The reference's cycle walk, swap
+        for swap, runs on positions (:func:`_cycle_walk`), then one gather moves the
+        ciphertexts: new[i] = old[indexes[i]] for a permutation, and the reference's own result
+        (or index panic) for any other list."""
+        perm = _cycle_walk(_index_array(indexes), self.count)
+        g = self._gather(torch.from_numpy(perm))
         self.C, self.sign, self.exp = g.C, g.sign, g.exp
         self.lit = False
 

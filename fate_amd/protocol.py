@@ -203,11 +203,11 @@ class evaluator:
 
     @staticmethod
     def i_shuffle(pk: PK, a: EV, indices: torch.LongTensor) -> None:
-        a.i_shuffle(indices.tolist() if isinstance(indices, torch.Tensor) else indices)
+        a.i_shuffle(indices)  # a tensor is read as an array, not a Python list
 
     @staticmethod
     def shuffle(pk: PK, a: EV, indices: torch.LongTensor) -> EV:
-        return a.shuffle(indices.tolist() if isinstance(indices, torch.Tensor) else indices)
+        return a.shuffle(indices)
 
     @staticmethod
     def intervals_slice(a: EV, intervals: List[Tuple[int, int]]) -> EV:

@@ -538,3 +538,31 @@ def test_iupdate_into_fresh_zeros(env):
     want2 = [O.ct_zero() for _ in range(10 * stride)]
     O.iupdate_with_masks(opk, want2, other, idx2, masks, stride)
     assert host(pk, v2) == ref(want2)
+
+
+def test_shuffles_and_index_slices(env):
+    """i_shuffle / shuffle (lib.rs:473-497) against the oracle's cycle walk, for a permutation
+    and for index lists that are not one (duplicates, a longer list), with the indexes as a
+    list and as a tensor (the protocol's Shuffler hands over tensors); slice_indexes
+    (lib.rs:457-463) with repeats and its index panic."""
+    fx, sk, pk, coder, opk, cts = env
+    rng = random.Random(21)
+    data = cts[:40]
+    perm = list(range(40))
+    rng.shuffle(perm)
+    dup = [rng.randrange(40) for _ in range(43)]
+    for ix in (perm, dup):
+        want = list(data)
+        O.i_shuffle(want, ix)
+        v = dev_vec(pk, data)
+        got = v.shuffle(torch.tensor(ix))
+        assert host(pk, got) == ref(want)
+        assert host(pk, v) == ref(data)  # shuffle leaves its source alone
+        v.i_shuffle(ix)
+        assert host(pk, v) == ref(want)
+    with pytest.raises(P.PanicException, match="index out of bounds"):
+        dev_vec(pk, data).i_shuffle(perm[:30])
+    sel = [3, 3, 0, 39, 17]
+    assert host(pk, dev_vec(pk, data).slice_indexes(sel)) == ref([data[i] for i in sel])
+    with pytest.raises(P.PanicException, match="the len is 40 but the index is 40"):
+        dev_vec(pk, data).slice_indexes([1, 40, 41])

@@ -255,3 +255,44 @@ def test_interval_bounds_follow_the_reference():
     s, e = P._interval_array([(2, 5), (0, 0), (7, 9)])
     idx, rel = P._interval_items(s, e)
     assert idx.tolist() == [2, 3, 4, 7, 8] and rel.tolist() == [0, 1, 2, 0, 1]
+
+
+
+def _ref_i_shuffle(data, indexes):
+    """The oracle's transcription of the reference walk (oracle/paillier_oracle.py i_shuffle,
+    lib.rs:473-490), on a copy; IndexError where Rust panics."""
+    from oracle import paillier_oracle as O
+    data = list(data)
+    O.i_shuffle(data, indexes)
+    return data
+
+def test_i_shuffle_cycle_walk_matches_reference():
+    """i_shuffle's walk replayed on positions by the host helper equals the reference's walk on
+    the data for permutations (new[i] = old[indexes[i]]) and for any other index list
+    (duplicates, fixed points, longer lists); a short list or an index past the data panics
+    where the reference does (the first out-of-bounds access, with its message)."""
+    import random
+
+    from fate_amd import paillier as P
+    rng = random.Random(8)
+    for n in (1, 2, 7, 64, 1000):
+        perm = list(range(n))
+        rng.shuffle(perm)
+        got = P._cycle_walk(np.array(perm), n)
+        assert got.tolist() == _ref_i_shuffle(range(n), perm) == perm
+        for _ in range(20):
+            ix = [rng.randrange(n) for _ in range(n + rng.randrange(3))]
+            assert P._cycle_walk(np.array(ix), n).tolist() == _ref_i_shuffle(range(n), ix)
+    for ix, n in (([1, 2], 3), ([0, 5, 1], 3), ([2, 0, 7, 1], 4)):
+        try:
+            _ref_i_shuffle(range(n), ix)
+            raise AssertionError("the reference walk should fail")
+        except IndexError:
+            pass
+        with pytest.raises(P.PanicException, match="index out of bounds"):
+            P._cycle_walk(np.array(ix), n)
+    with pytest.raises(OverflowError):
+        P._index_array([3, -1])
+    with pytest.raises(TypeError):
+        P._index_array([1.5])
+    assert P._index_array(torch.tensor([4, 2])).tolist() == [4, 2]
