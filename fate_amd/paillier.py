@@ -884,7 +884,11 @@ class CiphertextVector:
 
     def iadd_vec(self, other: "CiphertextVector", sa: int, sb: int, size: Optional[int], pk: "PK") -> None:
         """``CiphertextVector::iadd_vec`` (lib.rs:634-677)."""
-        if size is None:
+        if size is None:  # self.data[sa..] zipped with other.data[sb..]: either start may panic
+            if sa > self.count:
+                raise PanicException(f"range start index {sa} out of range for slice of length {self.count}")
+            if sb > other.count:
+                raise PanicException(f"range start index {sb} out of range for slice of length {other.count}")
             size = min(self.count - sa, other.count - sb)
         else:
             if sa + size > self.count:
@@ -926,7 +930,11 @@ class CiphertextVector:
 
     def isub_vec(self, other: "CiphertextVector", sa: int, sb: int, size: Optional[int], pk: "PK") -> None:
         """``CiphertextVector::isub_vec`` (lib.rs:679-722)."""
-        if size is None:
+        if size is None:  # self.data[sa..] zipped with other.data[sb..]: either start may panic
+            if sa > self.count:
+                raise PanicException(f"range start index {sa} out of range for slice of length {self.count}")
+            if sb > other.count:
+                raise PanicException(f"range start index {sb} out of range for slice of length {other.count}")
             size = min(self.count - sa, other.count - sb)
         else:
             if sa + size > self.count:
@@ -973,6 +981,8 @@ class CiphertextVector:
         if sa == sb:
             if size is not None and sa + size > n:
                 raise RuntimeError(f"end index out of range: sa={sa}, s={size}, data_size={n}")
+            if size is None and sa > n:  # self.data[sa..]
+                raise PanicException(f"range start index {sa} out of range for slice of length {n}")
             end = n if size is None else sa + size
             if end <= sa:
                 return
@@ -988,6 +998,8 @@ class CiphertextVector:
         if size is not None and w0 + size > n:
             nm = "sb" if sa < sb else "sa"
             raise RuntimeError(f"end index out of range: {nm}={w0}, s={size}, data_size={n}")
+        if size is None and w0 > n:  # iadd_i_j(w0, r0, len - w0): the first data[w0] is out of bounds
+            raise PanicException(f"index out of bounds: the len is {n} but the index is {w0}")
         s = (n - w0) if size is None else size
         d = w0 - r0
         # data[w0+k] op= data[r0+k] for k ascending; reads of r0+k >= w0 see earlier writes:
@@ -1133,11 +1145,18 @@ class CiphertextVector:
         data[i+j] += data[i+j-step] for j ascending -- an inclusive scan with stride `step`,
         run as a Hillis-Steele scan (log2(chunk/step) rounds of the ct-add kernel)."""
         sizes = [int(c) for c in chunk_sizes]
+        step = int(step)
+        n = self.count
+        # the reference touches data[i + j] for j in step..size: a chunk no longer than the step
+        # touches nothing (even past the data), a longer one panics at its first index >= len
+        i = 0
+        for c in sizes:
+            if c > step and i + c > n:
+                raise PanicException(f"index out of bounds: the len is {n} but the index is {max(n, i + step)}")
+            i += c
         total = sum(sizes)
-        if total == 0 or step <= 0:
+        if total == 0 or step <= 0:  # step 0: each element adds the literal 1, i.e. stays
             return
-        if total > self.count:
-            raise PanicException(f"index out of bounds: the len is {self.count} but the index is {total - 1}")
         starts = torch.repeat_interleave(torch.tensor([0] + list(itertools.accumulate(sizes))[:-1]),
                                          torch.tensor(sizes))
         rel = torch.arange(total) - starts

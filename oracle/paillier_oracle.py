@@ -488,11 +488,17 @@ def iupdate_with_masks(pk, data, other, indexes, masks, stride):
 
 
 def chunking_cumsum_with_step(pk: PK, data: List[Ciphertext], chunk_sizes: List[int], step: int) -> None:
-    """``CiphertextVector::chunking_cumsum_with_step`` (:763-774), in place."""
+    """``CiphertextVector::chunking_cumsum_with_step`` (:763-774), in place, with its two
+    mem::replace swaps: for step > 0 that is data[i+j] = add(data[i+j], data[i+j-step]); for
+    step 0 the element is added to the swapped-in literal 1, so it stays as it was."""
+    placeholder = ct_zero()
     i = 0
     for cs in chunk_sizes:
         for j in range(step, cs):
-            data[i + j] = ct_add(pk, data[i + j], data[i + j - step])
+            x = i + j
+            placeholder, data[x] = data[x], placeholder
+            placeholder = ct_add(pk, placeholder, data[x - step])
+            placeholder, data[x] = data[x], placeholder
         i += cs
 
 

@@ -491,7 +491,7 @@ def test_empty_and_degenerate_vector_ops(env):
     want = list(data)
     O.iupdate(opk, want, data[:6], [[]] * 6, 2)
     assert host(pk, v) == ref(want)
-    for sizes, step in (([0, 5, 0, 7], 2), ([3, 9], 4), ([12], 12), ([], 1)):
+    for sizes, step in (([0, 5, 0, 7], 2), ([3, 9], 4), ([12], 12), ([], 1), ([10, 2, 1], 2), ([5, 7], 0)):
         v = dev_vec(pk, data)
         v.chunking_cumsum_with_step(pk, sizes, step)
         want = list(data)
