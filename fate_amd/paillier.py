@@ -1194,6 +1194,8 @@ class CiphertextVector:
         """``CiphertextVector::pack_squeeze`` (paillier.rs:241; lib.rs:439-450): per chunk of
         pack_num, acc = x0; acc = acc^(2^offset_bit) * y mod n^2 for each further y; exp 0."""
         n = self.count
+        if pack_num == 0:  # self.data.chunks(0)
+            raise PanicException("chunk size must be non-zero")
         nch = -(-n // pack_num) if pack_num > 0 else 0
         if 0 < nch <= WIDE_SQUEEZE_MAX_CHUNKS and pack_num > 1:
             # few chunks: the whole squeeze in one launch, one chunk per wave (fphe_pack_squeeze)

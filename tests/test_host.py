@@ -325,3 +325,13 @@ def test_open_ended_ranges_panic_as_the_reference():
     with pytest.raises(P.PanicException, match="the len is 10 but the index is 12"):
         a.chunking_cumsum_with_step(pk, [10, 9], 2)
     a.chunking_cumsum_with_step(pk, [2, 2, 2, 2, 2, 2, 1], 2)  # past the data, but no chunk longer than the step
+
+
+def test_pack_squeeze_zero_pack_num_panics():
+    """pack_squeeze's self.data.chunks(pack_num) (lib.rs:439-450) panics for 0, before any
+    device work."""
+    from fate_amd import paillier as P
+    v = P.CiphertextVector(torch.zeros((1, 128, 64), dtype=torch.int32), torch.zeros(64, dtype=torch.uint8),
+                           torch.zeros(64, dtype=torch.int32), 5)
+    with pytest.raises(P.PanicException, match="chunk size must be non-zero"):
+        v.pack_squeeze(0, 10, P.PK((1 << 1023) + 1155))
