@@ -45,6 +45,16 @@
 #endif
 #define FPHE_OCC_ADD __attribute__((amdgpu_waves_per_eu(FPHE_ADD_OCC)))
 #define FPHE_OCC_FOLD __attribute__((amdgpu_waves_per_eu(FPHE_FOLD_OCC)))
+// the balanced first fold level (k_segfold27) on its own: its occupancy, and whether it fetches
+// the next term's words during the current product (35 VGPRs held across it) or right before
+// its own product (nothing but index state across a product)
+#ifndef FPHE_SEGFOLD_OCC
+#define FPHE_SEGFOLD_OCC FPHE_FOLD_OCC
+#endif
+#ifndef FPHE_SEGFOLD_PF
+#define FPHE_SEGFOLD_PF 1
+#endif
+#define FPHE_OCC_SEGFOLD __attribute__((amdgpu_waves_per_eu(FPHE_SEGFOLD_OCC)))
 #define FPHE_OCC_ENC __attribute__((amdgpu_waves_per_eu(FPHE_ENC_OCC)))
 // code-shape switches of the vector-op kernels (A/B and fault bisection):
 // wave-uniform loop trip counts in SGPRs, and per-lane operand choice by loading both
