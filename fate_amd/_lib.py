@@ -177,7 +177,7 @@ def load_py() -> ctypes.PyDLL:
             raise NativeLibraryMissing(
                 f"{PY_LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
         lib = ctypes.PyDLL(PY_LIB_PATH)
-        lib.fphe_py_positions_lens.argtypes = [ctypes.py_object, vp]
+        lib.fphe_py_positions_lens.argtypes = [ctypes.py_object, vp, ctypes.c_int64]
         lib.fphe_py_positions_lens.restype = ctypes.c_int64
         lib.fphe_py_positions_fill.argtypes = [ctypes.py_object, vp, ctypes.c_int64]
         lib.fphe_py_positions_fill.restype = ctypes.c_int64

@@ -14,15 +14,26 @@
 #include <Python.h>
 #include <stdint.h>
 
-/* lens[i] = len(outer[i]) for i < len(outer) (lens has room for len(outer)); returns the sum */
-int64_t fphe_py_positions_lens(PyObject* outer, int64_t* lens) {
-  PyObject* o = PySequence_Fast(outer, "positions: a sequence of sequences is required");
+/* Both passes walk a private tuple snapshot of the outer sequence (PySequence_Tuple holds
+ * strong references).  An inner list of plain ints -- the usual case -- is read in place: no
+ * Python code can run while it is read.  Any other inner sequence, or one holding other
+ * integer types (whose __index__ may run Python code), is read from its own tuple snapshot. */
+
+/* lens[i] = len(outer[i]) for i < len(outer) (lens has room for cap entries: a list that grew
+ * since the caller sized it is an error); returns the sum */
+int64_t fphe_py_positions_lens(PyObject* outer, int64_t* lens, int64_t cap) {
+  PyObject* o = PySequence_Tuple(outer);
   if (!o) return -1;
-  const Py_ssize_t n = PySequence_Fast_GET_SIZE(o);
-  PyObject** items = PySequence_Fast_ITEMS(o);
+  const Py_ssize_t n = PyTuple_GET_SIZE(o);
+  if ((int64_t)n != cap) {
+    Py_DECREF(o);
+    PyErr_SetString(PyExc_RuntimeError, "positions changed while being read");
+    return -1;
+  }
   int64_t total = 0;
   for (Py_ssize_t i = 0; i < n; ++i) {
-    const Py_ssize_t k = PySequence_Size(items[i]);
+    PyObject* in = PyTuple_GET_ITEM(o, i);
+    const Py_ssize_t k = PyList_CheckExact(in) ? PyList_GET_SIZE(in) : PySequence_Size(in);
     if (k < 0) {
       Py_DECREF(o);
       return -1;
@@ -37,19 +48,38 @@ int64_t fphe_py_positions_lens(PyObject* outer, int64_t* lens) {
 /* pos[j] = the j-th listed position, sample-major as the reference walks them; `total` is
  * what fphe_py_positions_lens returned (a list that changed in between is an error) */
 int64_t fphe_py_positions_fill(PyObject* outer, int64_t* pos, int64_t total) {
-  PyObject* o = PySequence_Fast(outer, "positions: a sequence of sequences is required");
+  PyObject* o = PySequence_Tuple(outer);
   if (!o) return -1;
-  const Py_ssize_t n = PySequence_Fast_GET_SIZE(o);
-  PyObject** items = PySequence_Fast_ITEMS(o);
+  const Py_ssize_t n = PyTuple_GET_SIZE(o);
   int64_t j = 0;
   for (Py_ssize_t i = 0; i < n; ++i) {
-    PyObject* in = PySequence_Fast(items[i], "positions: each sample's positions must be a sequence");
+    PyObject* li = PyTuple_GET_ITEM(o, i);
+    if (PyList_CheckExact(li)) {  /* in place while every item is a plain int */
+      const Py_ssize_t k = PyList_GET_SIZE(li);
+      Py_ssize_t t = 0;
+      if (j + (int64_t)k <= total) {
+        for (; t < k; ++t) {
+          PyObject* v = PyList_GET_ITEM(li, t);
+          if (!PyLong_CheckExact(v)) break;
+          const long long x = PyLong_AsLongLong(v);
+          if (x == -1 && PyErr_Occurred()) {
+            Py_DECREF(o);
+            return -1;
+          }
+          pos[j + t] = (int64_t)x;
+        }
+        if (t == k) {
+          j += k;
+          continue;
+        }
+      }
+    }
+    PyObject* in = PySequence_Tuple(li);
     if (!in) {
       Py_DECREF(o);
       return -1;
     }
-    const Py_ssize_t k = PySequence_Fast_GET_SIZE(in);
-    PyObject** v = PySequence_Fast_ITEMS(in);
+    const Py_ssize_t k = PyTuple_GET_SIZE(in);
     if (j + (int64_t)k > total) {
       Py_DECREF(in);
       Py_DECREF(o);
@@ -57,7 +87,7 @@ int64_t fphe_py_positions_fill(PyObject* outer, int64_t* pos, int64_t total) {
       return -1;
     }
     for (Py_ssize_t t = 0; t < k; ++t) {
-      const long long x = PyLong_AsLongLong(v[t]);  /* __index__ for numpy integers */
+      const long long x = PyLong_AsLongLong(PyTuple_GET_ITEM(in, t)); /* __index__ for numpy ints */
       if (x == -1 && PyErr_Occurred()) {
         Py_DECREF(in);
         Py_DECREF(o);

@@ -1500,7 +1500,7 @@ def _position_lists(indexes) -> Tuple[np.ndarray, np.ndarray]:
         indexes = list(indexes)
     lib = _lib.load_py()
     lens = np.empty(len(indexes), dtype=np.int64)
-    total = lib.fphe_py_positions_lens(indexes, lens.ctypes.data)
+    total = lib.fphe_py_positions_lens(indexes, lens.ctypes.data, lens.size)
     pos = np.empty(total, dtype=np.int64)
     lib.fphe_py_positions_fill(indexes, pos.ctypes.data, total)
     return lens, pos
